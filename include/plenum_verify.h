@@ -1,0 +1,126 @@
+/*
+ * plenum_verify.h — C ABI of the MI355X batch Ed25519 request-verification engine
+ * (libplenum_verify.so). Plain pointers and sizes only; no torch/HIP types cross this boundary
+ * (streams are passed as void*). All functions return 0 on success and a negative PV_ERR_* code on
+ * infrastructure failure; a bad signature is NEVER an error, it is a 0 verdict bit. No exceptions
+ * cross the ABI; pv_last_error() describes the last failure of the calling thread.
+ *
+ * What each entry point replaces in the reference (swcurran/indy-plenum):
+ *   pv_verify_batch        the per-signature ctypes call chain
+ *                          stp_core/crypto/nacl_wrappers.py:232-242 Verifier.verify
+ *                          -> :86-108 VerifyKey.verify(signature + msg)
+ *                          -> libnacl.crypto_sign_open(sm, pk) (libnacl 1.6.1, setup.py:107-108)
+ *                          -> libsodium 1.0.18 crypto_sign_open, batched: request i is the byte
+ *                          string sm[sm_off[i] : sm_off[i+1]] (exactly the `signature + msg`
+ *                          concatenation the reference builds, so the sig/msg split point is
+ *                          libsodium's: the first 64 bytes) verified against pk[32 i : 32 i + 32].
+ *                          verdict bit i (LSB-first within each byte) = 1 iff crypto_sign_open
+ *                          would return 0 (libnacl would not raise ValueError).
+ *   pv_verify_batch_device the same on device-resident inputs (the hot path the benchmark times).
+ *   pv_b58decode_batch     base58.b58decode (PyPI base58, unpinned; setup.py:98-99) as called from
+ *                          plenum/server/client_authn.py:97 (signature) and
+ *                          plenum/common/verifier.py:27,37,50 (identifier / verkey).
+ *   pv_resolve_verkeys     plenum/common/verifier.py:24-50 DidVerifier key resolution (cryptonym,
+ *                          abbreviated '~' verkey expansion, full verkey) for a batch.
+ *   pv_comm_* / pv_allgather_verdicts
+ *                          new: the cross-GPU gather of per-shard verdict bitmaps (one RCCL
+ *                          all-gather over xGMI). The reference has no equivalent.
+ * Threading: the reference caller is the single-threaded asyncio Looper (stp_core/loop/looper.py);
+ * the library is synchronous per call and keeps one context per process (one GPU per process).
+ */
+#ifndef PLENUM_VERIFY_H
+#define PLENUM_VERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PV_OK 0
+#define PV_ERR_NO_DEVICE (-1)
+#define PV_ERR_ALLOC (-2)
+#define PV_ERR_LAUNCH (-3)
+#define PV_ERR_ARG (-4)
+#define PV_ERR_NOT_INIT (-5)
+#define PV_ERR_COMM (-6)
+#define PV_ERR_DECODE (-7)
+
+/* Bytes that must be readable past sm_off[n] in a device blob (SHA-512 reads whole 8-byte words). */
+#define PV_BLOB_SLACK 256
+
+/* ABI version of this header. */
+#define PV_ABI_VERSION 1
+int pv_abi_version(void);
+
+/* Number of visible GPUs (0 when none; never an error). */
+int pv_device_count(void);
+
+/* Bind this process to `device`, build the fixed-base table, allocate the workspace. Idempotent
+ * for the same device. */
+int pv_init(int device);
+void pv_shutdown(void);
+const char* pv_last_error(void);
+
+/* Host buffers in, host bitmap out (ceil(n/8) bytes). sm_off has n+1 entries, non-decreasing;
+ * offsets need no alignment (the library copies into its own pinned staging buffer). Synchronous. */
+int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
+                    uint8_t* verdict_bits);
+
+/* Device buffers in, device bitmap out. Requirements: d_sm 4-byte aligned and readable up to
+ * sm_off[n] + PV_BLOB_SLACK (records themselves need no alignment), d_pk 16-byte aligned,
+ * verdict_words holds ceil(n/64) 64-bit words. Enqueued on `stream` (a hipStream_t, NULL = the
+ * library stream); returns without synchronising. */
+int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
+                           uint64_t* d_verdict_words, void* stream);
+
+/* With pv_set_timing(1), every launch records HIP events on its stream around each kernel;
+ * pv_last_kernel_times returns the summed device time (ms) of the prep kernels (checks, SHA-512,
+ * decompression, table of -A multiples) and the scalar-multiplication kernels of the last call. */
+int pv_set_timing(int enable);
+int pv_last_kernel_times(double* prep_ms, double* msm_ms);
+
+/* Batched base58 decode (Bitcoin alphabet, PyPI base58 2.x b58decode semantics: trailing ASCII
+ * whitespace stripped, each leading '1' -> 0x00). Input: strings concatenated in `chars` with
+ * n+1 offsets. Output: out[i * out_stride ...], out_len[i] bytes, status[i] = 0 ok, 1 invalid
+ * character, 2 longer than out_stride. */
+int pv_b58decode_batch(const char* chars, const uint64_t* off, uint64_t n, uint8_t* out,
+                       uint64_t out_stride, uint32_t* out_len, uint8_t* status);
+
+/* base58.b58encode of data[0..len): writes min(cap, result) chars, returns the full encoded length. */
+int64_t pv_b58encode(const uint8_t* data, uint64_t len, char* out, uint64_t cap);
+
+/* Batched DidVerifier key resolution (plenum/common/verifier.py:24-50) for n (identifier, verkey)
+ * string pairs (concatenated + offsets; an empty identifier means None, has_verkey[i] = 0 means
+ * verkey None). pk_out receives 32-byte raw keys. status[i]:
+ *   0 ok, raw 32-byte key in pk_out
+ *   1 ValueError("'verkey' should be a non-empty string")
+ *   2 InvalidKey (key resolution failed: bad base58, wrong length, bad hex)
+ *   3 empty key: the stp_core Verifier has no key and verify() returns False
+ *   4 identifier is not valid base58 (b58decode raises ValueError in DidVerifier.__init__)
+ * has_verkey/pk_out/status are per request. */
+int pv_resolve_verkeys(const char* idr_chars, const uint64_t* idr_off, const char* vk_chars,
+                       const uint64_t* vk_off, const uint8_t* has_verkey, uint64_t n, uint8_t* pk_out,
+                       uint8_t* status);
+
+/* Multi-GPU: one process per GPU. pv_comm_unique_id on rank 0, broadcast the 128 bytes by any
+ * channel, pv_comm_init on every rank (after pv_init). pv_allgather_verdicts gathers
+ * words_per_rank 64-bit verdict words from every rank into d_all (nranks * words_per_rank) with
+ * one RCCL all-gather on `stream`. */
+int pv_comm_unique_id(uint8_t out[128]);
+int pv_comm_init(int nranks, int rank, const uint8_t id[128]);
+int pv_allgather_verdicts(const uint64_t* d_local, uint64_t words_per_rank, uint64_t* d_all, void* stream);
+void pv_comm_destroy(void);
+
+/* Device memory helpers so hosts without a GPU framework can stage data (bench, smoke). */
+int pv_dev_alloc(void** p, uint64_t bytes);
+int pv_dev_free(void* p);
+int pv_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
+int pv_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
+int pv_sync(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLENUM_VERIFY_H */

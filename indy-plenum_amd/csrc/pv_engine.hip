@@ -1,0 +1,466 @@
+// libplenum_verify: MI355X batch Ed25519 verification engine (kernels + device-side C ABI).
+//
+// One lane per request, 256-thread workgroups, two workgroups per CU (2 waves/SIMD: measured
+// v_mad_u64_u32 throughput saturates at >= 2 waves/SIMD, profiles/r01_isa_rates.jsonl). The grid is
+// a fixed number of workgroups that stride over the batch, so the per-lane HBM table of [j](-A)
+// (9 cached points x 160 B) is sized by resident lanes, not by the batch.
+//
+// Replaces (per request) stp_core/crypto/nacl_wrappers.py:108 libnacl.crypto_sign_open(sm, pk);
+// see include/plenum_verify.h for the ABI contract and verify_core.h for the arithmetic.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "btable.h"
+#include "verify_core.h"
+#include "../../include/plenum_verify.h"
+
+static constexpr int PV_BLOCK = 256;
+static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per kernel pair (workspace ~1.6 GB)
+
+// ---------------------------------------------------------------------------------------- device
+
+struct DevATab {
+    uint4* base;
+    uint64_t nslots;
+    uint64_t slot;
+    __device__ __forceinline__ void store(int j, const uint32_t w[40]) const {
+#pragma unroll
+        for (int q = 0; q < 10; q++)
+            base[(uint64_t)(j * 10 + q) * nslots + slot] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+    __device__ __forceinline__ void load(int j, uint32_t w[40]) const {
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            const uint4 v = base[(uint64_t)(j * 10 + q) * nslots + slot];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+    }
+};
+
+struct LdsBTab {
+    const uint32_t* base;  // LDS
+    __device__ __forceinline__ void load(int j, ge_niels& q) const {
+        const uint4* e = reinterpret_cast<const uint4*>(base + j * PV_BTAB_STRIDE);
+        uint32_t w[32];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint4 v = e[i];
+            w[4 * i] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            q.yplusx.v[i] = w[i];
+            q.yminusx.v[i] = w[10 + i];
+            q.xy2d.v[i] = w[20 + i];
+        }
+    }
+};
+
+// Request bytes at an arbitrary byte offset: aligned dword loads + v_alignbyte_b32 funnel shifts.
+struct DevMsg {
+    const uint32_t* ap;  // rec rounded down to 4 bytes
+    uint32_t sh;         // rec & 3
+    __device__ __forceinline__ uint32_t dw(uint64_t i) const {
+        return __builtin_amdgcn_alignbyte(ap[i + 1], ap[i], sh);
+    }
+    // little-endian bytes [8q, 8q + 8) of the record
+    __device__ __forceinline__ uint64_t operator()(uint64_t q) const {
+        return ((uint64_t)dw(2 * q + 1) << 32) | dw(2 * q);
+    }
+};
+
+// Per-request intermediate state between the two kernels (SoA, coalesced per wave):
+//   atab  [9 entries][10 quads][n] uint4   cached [j](-A), j = 0..8
+//   digits[16][n] uint32                    radix-16 digits of k (8 words), radix-256 of S (8 words)
+//   flags [n] uint32                        1 = every libsodium pre-check passed
+struct Work {
+    uint4* atab;
+    uint32_t* digits;
+    uint32_t* flags;
+    uint64_t stride;  // chunk capacity (requests)
+};
+
+// Kernel 1: checks, decompression of A, k = SHA-512(R||A||M) mod L, table of [j](-A), recoding.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __restrict__ sm,
+                                                               const uint64_t* __restrict__ off, uint64_t n,
+                                                               const uint8_t* __restrict__ pk, Work wk) {
+    const uint64_t i = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o0 = off[i], o1 = off[i + 1];
+    const uint64_t smlen = o1 - o0;
+    const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
+    const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+    pv_sig_words in;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        in.R[q] = mw.dw(q);
+        in.S[q] = mw.dw(8 + q);
+    }
+    const uint4* pk4 = reinterpret_cast<const uint4*>(pk + 32 * i);
+    const uint4 a0 = pk4[0], a1 = pk4[1];
+    in.A[0] = a0.x; in.A[1] = a0.y; in.A[2] = a0.z; in.A[3] = a0.w;
+    in.A[4] = a1.x; in.A[5] = a1.y; in.A[6] = a1.z; in.A[7] = a1.w;
+
+    ge_p3 negA;
+    uint32_t k[8];
+    const bool ok = pv_prepare(negA, k, in, smlen, mw);
+    // -A goes to table slot 1 as an extended point; pv_table_kernel expands it to [j](-A)
+    uint32_t w[40];
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        w[q] = negA.X.v[q];
+        w[10 + q] = negA.Y.v[q];
+        w[20 + q] = negA.Z.v[q];
+        w[30 + q] = negA.T.v[q];
+    }
+    const DevATab at{wk.atab, wk.stride, i};
+    at.store(1, w);
+    uint32_t ek[8], fs[8];
+    sc_recode16(ek, k);
+    sc_recode256(fs, in.S);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        wk.digits[(uint64_t)q * wk.stride + i] = ek[q];
+        wk.digits[(uint64_t)(8 + q) * wk.stride + i] = fs[q];
+    }
+    wk.flags[i] = ok ? 1u : 0u;
+}
+
+// Kernel 1b: expand -A (extended, in slot 1) into the cached table [j](-A), j = 0..8.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk) {
+    const uint64_t i = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const DevATab at{wk.atab, wk.stride, i};
+    uint32_t w[40];
+    at.load(1, w);
+    ge_p3 negA;
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        negA.X.v[q] = w[q];
+        negA.Y.v[q] = w[10 + q];
+        negA.Z.v[q] = w[20 + q];
+        negA.T.v[q] = w[30 + q];
+    }
+    pv_build_a_table(at, negA);
+}
+
+// Kernel 2: Q = [S]B + [k](-A) by the regular-window Straus loop, encode, compare with R, ballot.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_msm_kernel(const uint8_t* __restrict__ sm,
+                                                              const uint64_t* __restrict__ off, uint64_t n,
+                                                              const uint32_t* __restrict__ btab_g, Work wk,
+                                                              uint64_t* __restrict__ verdict) {
+    __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
+    for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
+        reinterpret_cast<uint4*>(sbt)[t] = reinterpret_cast<const uint4*>(btab_g)[t];
+    __syncthreads();
+    const uint64_t i0 = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
+    const bool active = i0 < n;
+    const uint64_t i = active ? i0 : n - 1;
+    const DevATab at{wk.atab, wk.stride, i};
+    const LdsBTab bt{sbt};
+    uint32_t ek[8], fs[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        ek[q] = wk.digits[(uint64_t)q * wk.stride + i];
+        fs[q] = wk.digits[(uint64_t)(8 + q) * wk.stride + i];
+    }
+    uint32_t enc[8];
+    pv_straus(enc, at, bt, ek, fs);
+    const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[i]);
+    const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+    uint32_t R[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) R[q] = mw.dw(q);
+    const bool ok = active && wk.flags[i] != 0 && pv_words_equal(enc, R);
+    const uint64_t bits = __ballot(ok);
+    if ((threadIdx.x & 63) == 0 && i0 < n) verdict[i0 >> 6] = bits;
+}
+
+// ------------------------------------------------------------------------------------------ host
+
+namespace {
+
+struct Ctx {
+    int device = -1;
+    int cus = 0;
+    hipStream_t stream = nullptr;
+    uint32_t* d_btab = nullptr;
+    Work work{nullptr, nullptr, nullptr, 0};
+    // host-entry staging
+    uint8_t* h_stage = nullptr;  // pinned
+    uint64_t h_stage_cap = 0;
+    uint8_t* d_stage = nullptr;
+    uint64_t d_stage_cap = 0;
+    bool timing = false;
+    // per-chunk event triples (prep start, msm start, msm end) of the last launch
+    std::vector<hipEvent_t> ev;
+    int ev_used = 0;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+Ctx g_ctx;
+std::mutex g_mu;
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define PV_HIP(call, code)                                                                     \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess) return fail(code, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int ensure_stage(uint64_t host_bytes, uint64_t dev_bytes) {
+    if (host_bytes > g_ctx.h_stage_cap) {
+        if (g_ctx.h_stage) (void)hipHostFree(g_ctx.h_stage);
+        g_ctx.h_stage = nullptr;
+        const uint64_t cap = std::max<uint64_t>(host_bytes, 1 << 20);
+        PV_HIP(hipHostMalloc((void**)&g_ctx.h_stage, cap, hipHostMallocDefault), PV_ERR_ALLOC);
+        g_ctx.h_stage_cap = cap;
+    }
+    if (dev_bytes > g_ctx.d_stage_cap) {
+        if (g_ctx.d_stage) (void)hipFree(g_ctx.d_stage);
+        g_ctx.d_stage = nullptr;
+        const uint64_t cap = std::max<uint64_t>(dev_bytes, 1 << 20);
+        PV_HIP(hipMalloc((void**)&g_ctx.d_stage, cap), PV_ERR_ALLOC);
+        g_ctx.d_stage_cap = cap;
+    }
+    return PV_OK;
+}
+
+int ensure_events(int count) {
+    while ((int)g_ctx.ev.size() < count) {
+        hipEvent_t e;
+        PV_HIP(hipEventCreate(&e), PV_ERR_NO_DEVICE);
+        g_ctx.ev.push_back(e);
+    }
+    return PV_OK;
+}
+
+// Chunks of at most work.stride requests (a multiple of 64, so verdict words never straddle).
+int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk, uint64_t* d_verdict,
+           hipStream_t stream) {
+    if (n == 0) return PV_OK;
+    const uint64_t cap = g_ctx.work.stride;
+    const int nchunks = (int)((n + cap - 1) / cap);
+    if (g_ctx.timing) {
+        int rc = ensure_events(3 * nchunks);
+        if (rc) return rc;
+        g_ctx.ev_used = 3 * nchunks;
+    }
+    for (int c = 0; c < nchunks; c++) {
+        const uint64_t c0 = (uint64_t)c * cap;
+        const uint64_t m = std::min<uint64_t>(cap, n - c0);
+        const unsigned grid = (unsigned)((m + PV_BLOCK - 1) / PV_BLOCK);
+        if (g_ctx.timing) PV_HIP(hipEventRecord(g_ctx.ev[3 * c], stream), PV_ERR_LAUNCH);
+        hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+                           d_pk + 32 * c0, g_ctx.work);
+        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work);
+        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if (g_ctx.timing) PV_HIP(hipEventRecord(g_ctx.ev[3 * c + 1], stream), PV_ERR_LAUNCH);
+        hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+                           g_ctx.d_btab, g_ctx.work, d_verdict + c0 / 64);
+        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if (g_ctx.timing) PV_HIP(hipEventRecord(g_ctx.ev[3 * c + 2], stream), PV_ERR_LAUNCH);
+    }
+    return PV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pv_abi_version(void) { return PV_ABI_VERSION; }
+
+int pv_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* pv_last_error(void) { return g_err.c_str(); }
+
+int pv_init(int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ctx.device == device) return PV_OK;
+    if (g_ctx.device >= 0) return fail(PV_ERR_ARG, "pv_init: already bound to another device");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(PV_ERR_NO_DEVICE, "pv_init: no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(PV_ERR_ARG, "pv_init: device index out of range");
+    PV_HIP(hipSetDevice(device), PV_ERR_NO_DEVICE);
+    hipDeviceProp_t prop;
+    PV_HIP(hipGetDeviceProperties(&prop, device), PV_ERR_NO_DEVICE);
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(PV_ERR_NO_DEVICE, std::string("pv_init: built for gfx950, device is ") + prop.gcnArchName);
+    g_ctx.cus = prop.multiProcessorCount;
+    PV_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+    std::vector<uint32_t> bt(PV_BTAB_ENTRIES * PV_BTAB_STRIDE);
+    pv_build_b_table(bt.data());
+    PV_HIP(hipMalloc((void**)&g_ctx.d_btab, bt.size() * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMemcpy(g_ctx.d_btab, bt.data(), bt.size() * 4, hipMemcpyHostToDevice), PV_ERR_ALLOC);
+    const uint64_t S = PV_CHUNK;
+    g_ctx.work.stride = S;
+    PV_HIP(hipMalloc((void**)&g_ctx.work.atab, S * 9 * 160), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * 16 * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
+    g_ctx.device = device;
+    return PV_OK;
+}
+
+void pv_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ctx.device < 0) return;
+    if (g_ctx.comm) ncclCommDestroy(g_ctx.comm);
+    if (g_ctx.h_stage) (void)hipHostFree(g_ctx.h_stage);
+    if (g_ctx.d_stage) (void)hipFree(g_ctx.d_stage);
+    if (g_ctx.d_btab) (void)hipFree(g_ctx.d_btab);
+    if (g_ctx.work.atab) (void)hipFree(g_ctx.work.atab);
+    if (g_ctx.work.digits) (void)hipFree(g_ctx.work.digits);
+    if (g_ctx.work.flags) (void)hipFree(g_ctx.work.flags);
+    for (hipEvent_t e : g_ctx.ev) (void)hipEventDestroy(e);
+    if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
+    g_ctx = Ctx();
+}
+
+int pv_set_timing(int enable) {
+    g_ctx.timing = enable != 0;
+    return PV_OK;
+}
+
+int pv_last_kernel_times(double* prep_ms, double* msm_ms) {
+    if (!g_ctx.timing || g_ctx.device < 0 || g_ctx.ev_used == 0)
+        return fail(PV_ERR_ARG, "pv_last_kernel_times: timing disabled or nothing launched");
+    double p = 0, m = 0;
+    for (int c = 0; c < g_ctx.ev_used / 3; c++) {
+        float a = 0, b = 0;
+        PV_HIP(hipEventSynchronize(g_ctx.ev[3 * c + 2]), PV_ERR_LAUNCH);
+        PV_HIP(hipEventElapsedTime(&a, g_ctx.ev[3 * c], g_ctx.ev[3 * c + 1]), PV_ERR_LAUNCH);
+        PV_HIP(hipEventElapsedTime(&b, g_ctx.ev[3 * c + 1], g_ctx.ev[3 * c + 2]), PV_ERR_LAUNCH);
+        p += a;
+        m += b;
+    }
+    if (prep_ms) *prep_ms = p;
+    if (msm_ms) *msm_ms = m;
+    return PV_OK;
+}
+
+int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
+                           uint64_t* d_verdict_words, void* stream) {
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_verify_batch_device: call pv_init first");
+    if (n > 0 && (!d_sm || !d_off || !d_pk || !d_verdict_words)) return fail(PV_ERR_ARG, "null pointer");
+    return launch(d_sm, d_off, n, d_pk, d_verdict_words, stream ? (hipStream_t)stream : g_ctx.stream);
+}
+
+int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
+                    uint8_t* verdict_bits) {
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_verify_batch: call pv_init first");
+    if (n == 0) return PV_OK;
+    if (!sm || !sm_off || !pk || !verdict_bits) return fail(PV_ERR_ARG, "null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if (sm_off[i + 1] < sm_off[i]) return fail(PV_ERR_ARG, "sm_off must be non-decreasing");
+    std::lock_guard<std::mutex> lk(g_mu);
+    // staging layout (one pinned buffer, one device buffer, 256-B aligned sections):
+    //   [pk n*32][off (n+1) u64][verdict ceil(n/64) u64][blob + PV_BLOB_SLACK]
+    auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
+    const uint64_t pk_bytes = up(n * 32), off_bytes = up((n + 1) * 8), vwords = (n + 63) / 64;
+    const uint64_t v_bytes = up(vwords * 8);
+    const uint64_t blob = sm_off[n] - sm_off[0];
+    const uint64_t total = pk_bytes + off_bytes + v_bytes + blob + PV_BLOB_SLACK;
+    int rc = ensure_stage(total, total);
+    if (rc) return rc;
+    uint8_t* h = g_ctx.h_stage;
+    memcpy(h, pk, n * 32);
+    uint64_t* hoff = reinterpret_cast<uint64_t*>(h + pk_bytes);
+    for (uint64_t i = 0; i <= n; i++) hoff[i] = sm_off[i] - sm_off[0];
+    uint8_t* hblob = h + pk_bytes + off_bytes + v_bytes;
+    memcpy(hblob, sm + sm_off[0], blob);
+    memset(hblob + blob, 0, PV_BLOB_SLACK);
+    uint8_t* d = g_ctx.d_stage;
+    hipStream_t s = g_ctx.stream;
+    PV_HIP(hipMemcpyAsync(d, h, pk_bytes + off_bytes, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    PV_HIP(hipMemcpyAsync(d + pk_bytes + off_bytes + v_bytes, hblob, blob + PV_BLOB_SLACK,
+                          hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    uint64_t* dver = reinterpret_cast<uint64_t*>(d + pk_bytes + off_bytes);
+    rc = launch(d + pk_bytes + off_bytes + v_bytes, reinterpret_cast<const uint64_t*>(d + pk_bytes), n, d, dver, s);
+    if (rc) return rc;
+    uint64_t* hver = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
+    PV_HIP(hipMemcpyAsync(hver, dver, vwords * 8, hipMemcpyDeviceToHost, s), PV_ERR_LAUNCH);
+    PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
+    memcpy(verdict_bits, hver, (n + 7) / 8);  // little-endian words, LSB-first bits
+    return PV_OK;
+}
+
+int pv_comm_unique_id(uint8_t out[128]) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return fail(PV_ERR_COMM, "ncclGetUniqueId failed");
+    static_assert(sizeof(id.internal) == 128, "ncclUniqueId size");
+    memcpy(out, id.internal, 128);
+    return PV_OK;
+}
+
+int pv_comm_init(int nranks, int rank, const uint8_t id_bytes[128]) {
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_comm_init: call pv_init first");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PV_ERR_ARG, "pv_comm_init: bad rank");
+    ncclUniqueId id;
+    memcpy(id.internal, id_bytes, 128);
+    ncclResult_t r = ncclCommInitRank(&g_ctx.comm, nranks, id, rank);
+    if (r != ncclSuccess) return fail(PV_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    g_ctx.nranks = nranks;
+    g_ctx.rank = rank;
+    return PV_OK;
+}
+
+int pv_allgather_verdicts(const uint64_t* d_local, uint64_t words_per_rank, uint64_t* d_all, void* stream) {
+    if (!g_ctx.comm) return fail(PV_ERR_NOT_INIT, "pv_allgather_verdicts: call pv_comm_init first");
+    ncclResult_t r = ncclAllGather(d_local, d_all, words_per_rank, ncclUint64, g_ctx.comm,
+                                   stream ? (hipStream_t)stream : g_ctx.stream);
+    if (r != ncclSuccess) return fail(PV_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    return PV_OK;
+}
+
+void pv_comm_destroy(void) {
+    if (g_ctx.comm) ncclCommDestroy(g_ctx.comm);
+    g_ctx.comm = nullptr;
+}
+
+int pv_dev_alloc(void** p, uint64_t bytes) {
+    PV_HIP(hipMalloc(p, std::max<uint64_t>(bytes, 16)), PV_ERR_ALLOC);
+    return PV_OK;
+}
+int pv_dev_free(void* p) {
+    PV_HIP(hipFree(p), PV_ERR_ALLOC);
+    return PV_OK;
+}
+int pv_memcpy_h2d(void* dst, const void* src, uint64_t bytes) {
+    PV_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), PV_ERR_LAUNCH);
+    return PV_OK;
+}
+int pv_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
+    PV_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
+    return PV_OK;
+}
+int pv_sync(void) {
+    PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
+    return PV_OK;
+}
+
+}  // extern "C"

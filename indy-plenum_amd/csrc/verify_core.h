@@ -1,0 +1,223 @@
+// One Ed25519 verification per lane: libsodium 1.0.18 crypto_sign_open acceptance, bit-exact.
+//
+// Reference path: stp_core/crypto/nacl_wrappers.py:232-242 Verifier.verify
+// -> VerifyKey.verify(signature + msg) (:86-108) -> libnacl.crypto_sign_open(sm, pk) -> libsodium
+// crypto_sign_ed25519_open -> crypto_sign_ed25519_verify_detached.
+//
+// Pipeline per request (all integer VALU work):
+//   1. checks: smlen >= 64, S < L, R and A not small-order, A canonical      (bytewise)
+//   2. A' = -A by decompression (one x^((p-5)/8) chain)                       (~265 field ops)
+//   3. k = SHA-512(R || A || M) mod L                                         (3 compressions @ 299 B)
+//   4. Q = [S]B + [k]A' by a Straus double-scalar multiplication with regular windows: signed
+//      radix-16 digits of k against a 9-entry table of [j]A' (cached form, per-lane, in HBM),
+//      signed radix-256 digits of S against a 129-entry niels table of [j]B (LDS). Regular windows
+//      keep all 64 lanes of a wave on one instruction stream (sliding windows would diverge).
+//   5. accept iff encode(Q) == R bytewise (one inversion, canonical encoding).
+// The table/B-table storage is a template parameter so the same code runs on the host in tests.
+#pragma once
+#include "fe25519.h"
+#include "ge25519.h"
+#include "sc25519.h"
+#include "sha512.h"
+
+// The 7 small-order encodings libsodium 1.0.18 rejects (ge25519_has_small_order), as words.
+static constexpr uint32_t PV_BLACKLIST[7][8] = {
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du},
+    {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u},
+    {0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+    {0xffffffedu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu},
+    {0xffffffeeu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu}};
+
+PV_HD bool pv_has_small_order(const uint32_t s[8]) {
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        uint32_t diff = 0;
+#pragma unroll
+        for (int i = 0; i < 7; i++) diff |= s[i] ^ PV_BLACKLIST[k][i];
+        diff |= (s[7] & 0x7fffffffu) ^ PV_BLACKLIST[k][7];
+        any |= diff == 0;
+    }
+    return any;
+}
+
+// libsodium ge25519_is_canonical: false iff y in [p, 2^255) (top bit ignored)
+PV_HD bool pv_ge_is_canonical(const uint32_t s[8]) {
+    uint32_t all = s[1] & s[2] & s[3] & s[4] & s[5] & s[6];
+    const bool top = ((s[7] & 0x7fffffffu) == 0x7fffffffu) && all == 0xffffffffu;
+    const bool low = s[0] >= 0xffffffedu;
+    return !(top && low);
+}
+
+struct pv_sig_words {
+    uint32_t R[8], S[8], A[8];
+};
+
+PV_HD void ge_cached_store_words(uint32_t w[40], const ge_cached& c) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        w[i] = c.YplusX.v[i];
+        w[10 + i] = c.YminusX.v[i];
+        w[20 + i] = c.Z2.v[i];
+        w[30 + i] = c.T2d.v[i];
+    }
+}
+PV_HD void ge_cached_load_words(ge_cached& c, const uint32_t w[40]) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        c.YplusX.v[i] = w[i];
+        c.YminusX.v[i] = w[10 + i];
+        c.Z2.v[i] = w[20 + i];
+        c.T2d.v[i] = w[30 + i];
+    }
+}
+
+// Build the 9-entry table of [j](-A), j = 0..8, in cached form (entry 0 = identity).
+template <class ATab>
+PV_HD void pv_build_a_table(ATab& tab, const ge_p3& negA) {
+    ge_cached c, c1;
+    uint32_t w[40];
+    ge_cached_identity(c);
+    ge_cached_store_words(w, c);
+    tab.store(0, w);
+    ge_p3_to_cached(c1, negA);
+    ge_cached_store_words(w, c1);
+    tab.store(1, w);
+    ge_p1p1 t;
+    ge_p3 cur;
+    ge_p2_dbl(t, negA.X, negA.Y, negA.Z);
+    ge_p1p1_to_p3(cur, t);
+    ge_p3_to_cached(c, cur);
+    ge_cached_store_words(w, c);
+    tab.store(2, w);
+#pragma nounroll
+    for (int j = 3; j <= 8; j++) {
+        ge_add_cached(t, cur, c1);
+        ge_p1p1_to_p3(cur, t);
+        ge_p3_to_cached(c, cur);
+        ge_cached_store_words(w, c);
+        tab.store(j, w);
+    }
+}
+
+// Signed 4-bit digit at the top of a packed 256-bit nibble string, then shift it out.
+PV_HD int pv_take_top4(uint32_t e[8]) {
+    const int d = ((int32_t)e[7]) >> 28;
+#pragma unroll
+    for (int i = 7; i > 0; i--) e[i] = (e[i] << 4) | (e[i - 1] >> 28);
+    e[0] <<= 4;
+    return d;
+}
+PV_HD int pv_take_top8(uint32_t f[8]) {
+    const int d = ((int32_t)f[7]) >> 24;
+#pragma unroll
+    for (int i = 7; i > 0; i--) f[i] = (f[i] << 8) | (f[i - 1] >> 24);
+    f[0] <<= 8;
+    return d;
+}
+
+// Q = [S]B + [k]A' (A' = -A, tabulated) from the packed signed digits of k (ek, radix 16) and
+// S (fs, radix 256); returns encode(Q) in out[8]. ek/fs are consumed.
+template <class ATab, class BTab>
+PV_HD void pv_straus(uint32_t out[8], ATab& atab, BTab& btab, uint32_t ek[8], uint32_t fs[8]) {
+    ge_p3 acc;
+    ge_p3_identity(acc);
+    ge_p1p1 t;
+    fe X, Y, Z;
+    uint32_t w[40];
+    for (int win = 63; win >= 0; win--) {
+        const int e = pv_take_top4(ek);
+        if (win != 63) {
+            for (int j = 0; j < 3; j++) {
+                ge_p2_dbl(t, X, Y, Z);
+                ge_p1p1_to_p2(X, Y, Z, t);
+            }
+            ge_p2_dbl(t, X, Y, Z);
+            ge_p1p1_to_p3(acc, t);
+        }
+        ge_cached ca;
+        atab.load(e < 0 ? -e : e, w);
+        ge_cached_load_words(ca, w);
+        ge_cached_cneg(ca, e < 0);
+        ge_add_cached(t, acc, ca);
+        if ((win & 1) == 0) {
+            const int f = pv_take_top8(fs);
+            ge_p1p1_to_p3(acc, t);
+            ge_niels nb;
+            btab.load(f < 0 ? -f : f, nb);
+            ge_niels_cneg(nb, f < 0);
+            ge_add_niels(t, acc, nb);
+        }
+        ge_p1p1_to_p2(X, Y, Z, t);
+    }
+    ge_p2_tobytes(out, X, Y, Z);
+}
+
+template <class ATab, class BTab>
+PV_HD void pv_double_scalarmult(uint32_t out[8], ATab& atab, BTab& btab, const uint32_t k[8],
+                                const uint32_t S[8]) {
+    uint32_t ek[8], fs[8];
+    sc_recode16(ek, k);
+    sc_recode256(fs, S);
+    pv_straus(out, atab, btab, ek, fs);
+}
+
+// Stage 1 of a verification: the checks, A decompression and k. Returns false if any libsodium
+// pre-check rejects (the caller still runs the arithmetic on harmless data and masks the verdict).
+template <class MsgWord>
+PV_HD bool pv_prepare(ge_p3& negA, uint32_t k[8], const pv_sig_words& in, uint64_t smlen,
+                      const MsgWord& msgword) {
+    bool ok = smlen >= 64;
+    ok &= sc_is_canonical(in.S);
+    ok &= !pv_has_small_order(in.R);
+    ok &= pv_ge_is_canonical(in.A);
+    ok &= !pv_has_small_order(in.A);
+    ok &= ge_frombytes_negate(negA, in.A);
+
+    // SHA-512 over R || A || M: the input is sm with bytes 32..63 (S) replaced by A, so SHA word
+    // q >= 8 is sm word q; T = smlen bytes in total.
+    const uint64_t T = smlen;
+    uint64_t st[8];
+    sha512_init(st);
+    const uint64_t nblocks = (T + 17 + 127) / 128;
+    for (uint64_t b = 0; b < nblocks; b++) {
+        uint64_t blk[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint64_t q = 16 * b + j;
+            uint64_t raw;  // little-endian bytes 8q..8q+7 of the SHA input
+            if (q < 4) raw = ((uint64_t)in.R[2 * q + 1] << 32) | in.R[2 * q];
+            else if (q < 8) raw = ((uint64_t)in.A[2 * (q - 4) + 1] << 32) | in.A[2 * (q - 4)];
+            else raw = (8 * q < T) ? msgword(q) : 0;
+            const uint64_t pos = 8 * q;
+            if (pos + 8 > T) {
+                // bytes at or beyond T: keep the data bytes, then 0x80, then zeros
+                const uint64_t nb = (pos >= T) ? 0 : T - pos;  // data bytes in this word (0..7)
+                raw = (nb == 0) ? 0 : (raw & ((1ULL << (8 * nb)) - 1));
+                if (pos <= T) raw |= 0x80ULL << (8 * nb);
+            }
+            uint64_t be = pv_bswap64(raw);
+            if (b == nblocks - 1 && j == 15) be = T * 8;  // bit length (upper 64 bits are zero)
+            blk[j] = be;
+        }
+        sha512_compress(st, blk);
+    }
+    uint32_t h[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t le = pv_bswap64(st[i]);
+        h[2 * i] = (uint32_t)le;
+        h[2 * i + 1] = (uint32_t)(le >> 32);
+    }
+    sc_reduce64(k, h);
+    return ok;
+}
+
+PV_HD bool pv_words_equal(const uint32_t a[8], const uint32_t b[8]) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) d |= a[i] ^ b[i];
+    return d == 0;
+}

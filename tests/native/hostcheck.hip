@@ -1,0 +1,89 @@
+// TEST INFRASTRUCTURE: host-compiled build of the device arithmetic headers
+// (indy-plenum_amd/csrc/*.h) with PV_BOUNDS_CHECK, so tests can drive the exact kernel code on the
+// CPU against Python big integers, the C oracle and libsodium. Not part of the product library.
+#define PV_BOUNDS_CHECK 1
+#include "verify_core.h"
+#include "btable.h"
+#include <string.h>
+#include <vector>
+
+extern "C" {
+
+static void load_words(uint32_t w[8], const uint8_t* b) { memcpy(w, b, 32); }
+
+// raw limb ops (limbs supplied by the caller, so bound assertions are exercised)
+void hc_fe_mul(uint32_t* h, const uint32_t* f, const uint32_t* g) {
+    fe a, b, c; memcpy(a.v, f, 40); memcpy(b.v, g, 40); fe_mul(c, a, b); memcpy(h, c.v, 40);
+}
+void hc_fe_sq(uint32_t* h, const uint32_t* f) {
+    fe a, c; memcpy(a.v, f, 40); fe_sq(c, a); memcpy(h, c.v, 40);
+}
+void hc_fe_carry(uint32_t* h, const uint32_t* f) {
+    fe a, c; memcpy(a.v, f, 40); fe_carry(c, a); memcpy(h, c.v, 40);
+}
+void hc_fe_tobytes(uint8_t* s, const uint32_t* f) {
+    fe a; memcpy(a.v, f, 40); uint32_t w[8]; fe_tobytes32(w, a); memcpy(s, w, 32);
+}
+void hc_fe_frombytes(uint32_t* h, const uint8_t* s) {
+    uint32_t w[8]; load_words(w, s); fe a; fe_frombytes32(a, w); memcpy(h, a.v, 40);
+}
+void hc_fe_invert(uint32_t* h, const uint32_t* f) {
+    fe a, c; memcpy(a.v, f, 40); fe_invert(c, a); memcpy(h, c.v, 40);
+}
+void hc_fe_pow22523(uint32_t* h, const uint32_t* f) {
+    fe a, c; memcpy(a.v, f, 40); fe_pow22523(c, a); memcpy(h, c.v, 40);
+}
+void hc_sc_reduce64(uint8_t* r, const uint8_t* x) {
+    uint32_t xw[16], rw[8]; memcpy(xw, x, 64); sc_reduce64(rw, xw); memcpy(r, rw, 32);
+}
+int hc_sc_is_canonical(const uint8_t* s) { uint32_t w[8]; load_words(w, s); return sc_is_canonical(w); }
+void hc_sc_recode16(uint8_t* out, const uint8_t* a) { uint32_t w[8], o[8]; load_words(w, a); sc_recode16(o, w); memcpy(out, o, 32); }
+void hc_sc_recode256(uint8_t* out, const uint8_t* a) { uint32_t w[8], o[8]; load_words(w, a); sc_recode256(o, w); memcpy(out, o, 32); }
+int hc_has_small_order(const uint8_t* s) { uint32_t w[8]; load_words(w, s); return pv_has_small_order(w); }
+int hc_ge_is_canonical(const uint8_t* s) { uint32_t w[8]; load_words(w, s); return pv_ge_is_canonical(w); }
+
+void hc_build_b_table(uint32_t* out) { pv_build_b_table(out); }
+
+struct HostATab {
+    uint32_t e[9][40];
+    void store(int j, const uint32_t w[40]) { memcpy(e[j], w, 160); }
+    void load(int j, uint32_t w[40]) const { memcpy(w, e[j], 160); }
+};
+
+struct HostMsg {
+    const uint8_t* sm;
+    uint64_t operator()(uint64_t q) const { uint64_t v; memcpy(&v, sm + 8 * q, 8); return v; }
+};
+
+// Full pipeline on the host: crypto_sign_open(sm, smlen, pk) == 0 ? 1 : 0.
+// sm must be readable for smlen + 8 bytes (the kernel contract: record slack).
+int hc_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    static std::vector<uint32_t> btab;
+    if (btab.empty()) { btab.resize(PV_BTAB_ENTRIES * PV_BTAB_STRIDE); pv_build_b_table(btab.data()); }
+    std::vector<uint8_t> buf(smlen + 80, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    ge_p3 negA; uint32_t k[8];
+    HostMsg mw{buf.data()};
+    bool ok = pv_prepare(negA, k, in, smlen, mw);
+    HostATab at;
+    pv_build_a_table(at, negA);
+    pv_btab_flat bt{btab.data()};
+    uint32_t enc[8];
+    pv_double_scalarmult(enc, at, bt, k, in.S);
+    return ok && pv_words_equal(enc, in.R);
+}
+
+// k = SHA-512(R||A||M) mod L through pv_prepare (exposes the hashing + reduction)
+void hc_prepare_k(uint8_t* kout, const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    std::vector<uint8_t> buf(smlen + 80, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in; memcpy(in.R, buf.data(), 32); memcpy(in.S, buf.data() + 32, 32); memcpy(in.A, pk, 32);
+    ge_p3 negA; uint32_t k[8]; HostMsg mw{buf.data()};
+    pv_prepare(negA, k, in, smlen, mw);
+    memcpy(kout, k, 32);
+}
+}

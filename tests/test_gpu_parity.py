@@ -1,0 +1,64 @@
+"""GPU parity: the HIP engine's verdicts vs libsodium 1.0.18 (the reference's own native verifier,
+nacl_wrappers.py:108) and the C oracle, on seeded normal + adversarial vectors. Calls go through
+the C ABI (libplenum_verify.so) via plenum_amd._native."""
+import numpy as np
+import pytest
+
+from vectors import VectorGen, pack
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def native():
+    from plenum_amd import _native
+    _native.ensure_device()
+    return _native
+
+
+def reference_verdicts(sodium, cases):
+    return np.array([sodium.sign_open_ok(sm, pk) for sm, pk in cases], dtype=bool)
+
+
+def test_each_adversarial_class(native, sodium, oracle):
+    g = VectorGen(sodium, oracle, seed=11)
+    cases = []
+    for cls in VectorGen.CLASSES:
+        cases += [g.make(cls) for _ in range(24)]
+    blob, off, pks = pack(cases)
+    got = native.verify_sm_batch(blob, off, pks)
+    want = reference_verdicts(sodium, cases)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(VectorGen.CLASSES[i // 24], cases[i][0].hex(), cases[i][1].hex(), want[i]) for i in bad[:5]]
+    # the classes that must be rejected are, and mixed-order keys pass ~1/8 of the time
+    assert want.sum() > 24 * 3
+
+
+def test_mixed_batch_2pct(native, sodium, oracle):
+    g = VectorGen(sodium, oracle, seed=12)
+    cases = g.batch(3000, adversarial_frac=0.02)
+    blob, off, pks = pack(cases)
+    got = native.verify_sm_batch(blob, off, pks)
+    want = reference_verdicts(sodium, cases)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
+def test_unaligned_offsets_and_ragged(native, sodium, oracle):
+    g = VectorGen(sodium, oracle, seed=13)
+    cases = [g.valid(g.msg(0, 300)) for _ in range(200)] + [g.make("short_sm") for _ in range(20)]
+    g.rng.shuffle(cases)
+    # leading garbage so that record starts are at every residue mod 8
+    blob, off, pks = pack(cases)
+    blob2 = np.concatenate([np.full(3, 0xAA, np.uint8), blob])
+    got = native.verify_sm_batch(blob2, off + 3, pks)
+    want = reference_verdicts(sodium, cases)
+    assert np.array_equal(got, want)
+
+
+def test_empty_and_single(native, sodium, oracle):
+    g = VectorGen(sodium, oracle, seed=14)
+    assert native.verify_sm_batch(np.zeros(0, np.uint8), np.zeros(1, np.uint64), np.zeros((0, 32), np.uint8)).size == 0
+    for n in (1, 63, 64, 65, 257):
+        cases = g.batch(n, adversarial_frac=0.3)
+        blob, off, pks = pack(cases)
+        assert np.array_equal(native.verify_sm_batch(blob, off, pks), reference_verdicts(sodium, cases))

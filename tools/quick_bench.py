@@ -1,0 +1,37 @@
+"""Quick device-resident throughput probe (development tool; bench.py is the contract)."""
+import ctypes, os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "indy-plenum_amd"), os.path.join(ROOT, "tests")]
+from plenum_amd import _native
+from oracle.libsodium_ref import LibSodium
+ls = LibSodium()
+n_unique = int(os.environ.get("NU", "8192")); n = int(os.environ.get("N", str(1 << 20)))
+rng = np.random.default_rng(1)
+cases = []
+for i in range(n_unique):
+    pk, sk = ls.seed_keypair(rng.bytes(32))
+    m = rng.bytes(299)
+    cases.append((ls.sign_detached(m, sk) + m, pk))
+reps = n // n_unique
+blob = np.frombuffer(b"".join(sm for sm, _ in cases) * reps, np.uint8)
+pks = np.frombuffer(b"".join(pk for _, pk in cases) * reps, np.uint8)
+off = np.arange(n + 1, dtype=np.uint64) * 363
+_native.ensure_device()
+L = _native.lib()
+def dalloc(b):
+    p = ctypes.c_void_p(); _native.check(L.pv_dev_alloc(ctypes.byref(p), b), "alloc"); return p
+d_blob = dalloc(blob.nbytes + 256); d_off = dalloc(off.nbytes); d_pk = dalloc(pks.nbytes); d_v = dalloc((n + 63) // 64 * 8)
+L.pv_memcpy_h2d(d_blob, blob.ctypes.data, blob.nbytes); L.pv_memcpy_h2d(d_off, off.ctypes.data, off.nbytes); L.pv_memcpy_h2d(d_pk, pks.ctypes.data, pks.nbytes)
+L.pv_set_timing(1)
+for it in range(int(os.environ.get("IT", "3"))):
+    t = time.time()
+    _native.check(L.pv_verify_batch_device(d_blob, d_off, n, d_pk, d_v, None), "verify")
+    _native.check(L.pv_sync(), "sync")
+    dt = time.time() - t
+    pm, mm = ctypes.c_double(), ctypes.c_double()
+    L.pv_last_kernel_times(ctypes.byref(pm), ctypes.byref(mm))
+    v = np.zeros((n + 63) // 64, np.uint64); L.pv_memcpy_d2h(v.ctypes.data, d_v, v.nbytes)
+    ok = int(np.unpackbits(v.view(np.uint8), bitorder="little")[:n].sum())
+    print({"n": n, "wall_s": round(dt, 4), "verifies_per_s": round(n / dt), "prep_ms": round(pm.value, 2),
+           "msm_ms": round(mm.value, 2), "valid": ok}, flush=True)
