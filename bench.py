@@ -1,0 +1,263 @@
+"""bench.py — Ed25519 request verifies/sec on MI355X (BASELINE.json metric), one process per GPU.
+
+A step = one pass of the hot path over one batch: pv_verify_batch_device on this rank's shard of
+device-resident synthetic NYM-style signed requests (1M per GPU, configs[1] of BASELINE.json; weak
+scaling), and for N > 1 the one RCCL all-gather of the per-shard verdict bitmaps.
+Inputs are uploaded to HBM before the timed region; host serialization and PCIe are reported
+separately, never as `value`.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--per-gpu REQUESTS]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "indy-plenum_amd"), os.path.join(ROOT, "tools")]
+
+import bench_constants as BC  # noqa: E402
+import nym_workload  # noqa: E402
+from plenum_amd import _native  # noqa: E402
+
+METRIC = "Ed25519 request verifies/sec (1/2/4/8 MI355X) + % int-VALU peak"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class DeviceBatch:
+    """Device-resident copy of one shard (library-owned allocations, no framework tensors)."""
+
+    def __init__(self, blob, off, pks):
+        L = _native.lib()
+        self.n = len(off) - 1
+        self.ptrs = []
+        self.d_blob = self._put(blob, blob.nbytes + _native.PV_BLOB_SLACK)
+        self.d_off = self._put(off, off.nbytes)
+        self.d_pk = self._put(pks, pks.nbytes)
+        self.words = (self.n + 63) // 64
+        self.d_verdict = self._alloc(self.words * 8)
+        self.L = L
+
+    def _alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        _native.check(_native.lib().pv_dev_alloc(ctypes.byref(p), nbytes), "pv_dev_alloc")
+        self.ptrs.append(p)
+        return p
+
+    def _put(self, arr, nbytes):
+        p = self._alloc(nbytes)
+        arr = np.ascontiguousarray(arr)
+        _native.check(_native.lib().pv_memcpy_h2d(p, arr.ctypes.data, arr.nbytes), "pv_memcpy_h2d")
+        return p
+
+    def verify(self):
+        _native.check(self.L.pv_verify_batch_device(self.d_blob, self.d_off, self.n, self.d_pk, self.d_verdict, None),
+                      "pv_verify_batch_device")
+
+    def verdict_words(self, ptr=None, words=None):
+        words = words or self.words
+        out = np.zeros(words, dtype=np.uint64)
+        _native.check(self.L.pv_memcpy_d2h(out.ctypes.data, ptr or self.d_verdict, out.nbytes), "pv_memcpy_d2h")
+        return out
+
+    def free(self):
+        for p in self.ptrs:
+            self.L.pv_dev_free(p)
+
+
+def cpu_baseline(blob, off, pks, sample):
+    """libsodium 1.0.18 crypto_sign_open (the reference's verifier) on the host's cores, over the
+    first `sample` requests of the same workload; the C oracle if libsodium is absent."""
+    from oracle.libsodium_ref import find_libsodium
+    from oracle.oracle import Oracle
+    o = Oracle()
+    fn = o.lib.cpu_baseline_run
+    fn.restype = ctypes.c_int64
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_uint64, ctypes.c_int]
+    path = find_libsodium()
+    threads = min(16, len(os.sched_getaffinity(0)))
+    use_sodium = path is not None
+    if not use_sodium:
+        sample = min(sample, 2000)
+        threads = 1
+    off_s = np.ascontiguousarray(off[:sample + 1])
+    t0 = time.perf_counter()
+    acc = fn((path or "").encode(), 1 if use_sodium else 0, blob.ctypes.data, off_s.ctypes.data, pks.ctypes.data,
+             sample, threads)
+    dt = time.perf_counter() - t0
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        pass
+    return {"value": round(sample / dt, 1), "unit": "verifies/s", "cores": threads,
+            "kind": "reference" if use_sodium else "port",
+            "sample": "%d requests of the same synthetic NYM workload, crypto_sign_open on %d threads (%s), %s"
+                      % (sample, threads, cpu_model,
+                         "libsodium %s at %s" % ("1.0.18", path) if use_sodium else "C oracle restatement"),
+            "accepted": int(acc), "seconds": round(dt, 3)}
+
+
+def pmc_traffic():
+    """HBM bytes per pv_msm_kernel launch from the committed rocprofv3 PMC summary, if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_msm_latest.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--cpu-sample", type=int, default=400000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--dataset", default=None, help="npz from tools/nym_workload.py (profiling runs: no fork)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n = args.per_gpu
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    t0 = time.perf_counter()
+    if args.dataset and os.path.exists(args.dataset):
+        blob, off, pks, lo = nym_workload.load(args.dataset)
+        assert lo == rank * n and len(off) - 1 == n, "dataset does not match this rank's shard"
+    else:
+        blob, off, pks = nym_workload.generate(rank * n, n)
+    gen_s = time.perf_counter() - t0
+    log("rank %d: generated %d requests (%.1f MB) in %.1f s" % (rank, n, blob.nbytes / 1e6, gen_s))
+
+    _native.ensure_device(local_rank)
+    L = _native.lib()
+    db = DeviceBatch(blob, off, pks)
+    d_all = None
+    if world > 1:
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            _native.check(L.pv_comm_unique_id(uid), "pv_comm_unique_id")
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        _native.check(L.pv_comm_init(world, rank, uid), "pv_comm_init")
+        d_all = db._alloc(db.words * 8 * world)
+
+    def step():
+        db.verify()
+        if world > 1:
+            _native.check(L.pv_allgather_verdicts(db.d_verdict, db.words, d_all, None), "pv_allgather_verdicts")
+
+    def barrier_sync():
+        _native.check(L.pv_sync(), "pv_sync")
+        if world > 1:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync()
+    L.pv_set_timing(1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    prep_ms, table_ms, msm_ms, launches = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    _native.check(L.pv_kernel_times(ctypes.byref(prep_ms), ctypes.byref(table_ms), ctypes.byref(msm_ms),
+                                    ctypes.byref(launches)), "pv_kernel_times")
+    L.pv_set_timing(0)
+    if world > 1:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness of the timed work: every synthetic request is validly signed
+    local = np.unpackbits(db.verdict_words().view(np.uint8), bitorder="little")[:n]
+    ok_local = int(local.sum())
+    ok_all = None
+    if world > 1:
+        allw = db.verdict_words(d_all, db.words * world)
+        ok_all = int(np.unpackbits(allw.view(np.uint8), bitorder="little").sum())
+
+    total = n * world * args.steps
+    value = total / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+    k = max(1, launches.value)
+    msm_avg_ms = msm_ms.value / k
+    achieved = BC.MAC_MSM_KERNEL * n / (msm_avg_ms * 1e-3)
+    pipeline_ms = (prep_ms.value + table_ms.value + msm_ms.value) / k
+    per_gpu_rate = n / (pipeline_ms * 1e-3)
+
+    result = {
+        "metric": METRIC, "value": round(value, 1), "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "configs[1]: %d single-sig NYM-style requests per GPU (~299 B signing-serialized, "
+                               "1024 signer DIDs), device-resident" % n,
+                   "requests_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
+                   "record_bytes_avg": round(float(blob.nbytes) / n, 1)},
+        "roofline": {"bound": "valu", "kernel": "pv_msm_kernel",
+                     "achieved": round(achieved / 1e12, 3), "peak": round(BC.PEAK_MAC_PER_S / 1e12, 3),
+                     "unit": "TMAC/s (v_mad_u64_u32 int32 MACs)", "frac": round(achieved / BC.PEAK_MAC_PER_S, 4),
+                     "traffic": pmc_traffic(),
+                     "algorithmic_mac_per_verify": round(BC.MAC_MSM_KERNEL), "launch_ms": round(msm_avg_ms, 4)},
+        "pipeline": {"prep_ms": round(prep_ms.value / k, 4), "table_ms": round(table_ms.value / k, 4),
+                     "msm_ms": round(msm_avg_ms, 4), "kernel_verifies_per_s_per_gpu": round(per_gpu_rate, 1),
+                     "whole_verify_valu_frac": round(BC.MAC_PER_VERIFY * per_gpu_rate / BC.PEAK_MAC_PER_S, 4),
+                     "hbm_staging_GBps": round(BC.ALGO_BYTES_PER_VERIFY * per_gpu_rate / 1e9, 2)},
+        "verdicts_ok": ok_local == n and (ok_all is None or ok_all == n * world),
+    }
+    if rank == 0 and world == 1 and not args.no_host_path:
+        # PCIe-inclusive host-buffer path (pv_verify_batch): staging copy + H2D + kernels + D2H
+        hsamp = min(n, 1 << 18)
+        hoff = off[:hsamp + 1]
+        _native.verify_sm_batch(blob[:int(hoff[-1])], hoff, pks[:hsamp])
+        t1 = time.perf_counter()
+        v = _native.verify_sm_batch(blob[:int(hoff[-1])], hoff, pks[:hsamp])
+        dt = time.perf_counter() - t1
+        result["host_path"] = {"verifies_per_s": round(hsamp / dt, 1), "requests": hsamp, "ok": bool(v.all())}
+        result["host_prep"] = {"workload_generation_s": round(gen_s, 2), "note": "serialize + sign, %d workers" % min(
+            16, os.cpu_count() or 1)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(blob, off, pks, min(args.cpu_sample, n))
+        result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    db.free()
+    if world > 1:
+        L.pv_comm_destroy()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

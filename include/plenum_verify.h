@@ -75,11 +75,13 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
 int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
                            uint64_t* d_verdict_words, void* stream);
 
-/* With pv_set_timing(1), every launch records HIP events on its stream around each kernel;
- * pv_last_kernel_times returns the summed device time (ms) of the prep kernels (checks, SHA-512,
- * decompression, table of -A multiples) and the scalar-multiplication kernels of the last call. */
+/* pv_set_timing(1) (re)starts timing: from then on every launch records HIP events on its own
+ * stream around each of its kernels. pv_kernel_times returns the device time (ms) summed over all
+ * kernel launches since then: prep (checks, SHA-512, reduction, decompression of A), table (the
+ * [j](-A) multiples) and msm (the Straus double-scalar multiplication + encode + compare), and the
+ * number of launches of each. pv_set_timing(0) stops recording. */
 int pv_set_timing(int enable);
-int pv_last_kernel_times(double* prep_ms, double* msm_ms);
+int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* launches);
 
 /* Batched base58 decode (Bitcoin alphabet, PyPI base58 2.x b58decode semantics: trailing ASCII
  * whitespace stripped, each leading '1' -> 0x00). Input: strings concatenated in `chars` with

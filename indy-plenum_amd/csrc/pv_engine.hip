@@ -205,7 +205,8 @@ struct Ctx {
     uint8_t* d_stage = nullptr;
     uint64_t d_stage_cap = 0;
     bool timing = false;
-    // per-chunk event triples (prep start, msm start, msm end) of the last launch
+    // event quadruples (prep start, table start, msm start, msm end), one per chunk launched since
+    // pv_set_timing(1); pv_kernel_times sums them
     std::vector<hipEvent_t> ev;
     int ev_used = 0;
     ncclComm_t comm = nullptr;
@@ -260,26 +261,30 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
     if (n == 0) return PV_OK;
     const uint64_t cap = g_ctx.work.stride;
     const int nchunks = (int)((n + cap - 1) / cap);
+    int evb = 0;
     if (g_ctx.timing) {
-        int rc = ensure_events(3 * nchunks);
+        evb = g_ctx.ev_used;
+        int rc = ensure_events(evb + 4 * nchunks);
         if (rc) return rc;
-        g_ctx.ev_used = 3 * nchunks;
+        g_ctx.ev_used = evb + 4 * nchunks;
     }
     for (int c = 0; c < nchunks; c++) {
         const uint64_t c0 = (uint64_t)c * cap;
         const uint64_t m = std::min<uint64_t>(cap, n - c0);
         const unsigned grid = (unsigned)((m + PV_BLOCK - 1) / PV_BLOCK);
-        if (g_ctx.timing) PV_HIP(hipEventRecord(g_ctx.ev[3 * c], stream), PV_ERR_LAUNCH);
+        hipEvent_t* e = g_ctx.timing ? &g_ctx.ev[evb + 4 * c] : nullptr;
+        if (e) PV_HIP(hipEventRecord(e[0], stream), PV_ERR_LAUNCH);
         hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                            d_pk + 32 * c0, g_ctx.work);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if (e) PV_HIP(hipEventRecord(e[1], stream), PV_ERR_LAUNCH);
         hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (g_ctx.timing) PV_HIP(hipEventRecord(g_ctx.ev[3 * c + 1], stream), PV_ERR_LAUNCH);
+        if (e) PV_HIP(hipEventRecord(e[2], stream), PV_ERR_LAUNCH);
         hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                            g_ctx.d_btab, g_ctx.work, d_verdict + c0 / 64);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (g_ctx.timing) PV_HIP(hipEventRecord(g_ctx.ev[3 * c + 2], stream), PV_ERR_LAUNCH);
+        if (e) PV_HIP(hipEventRecord(e[3], stream), PV_ERR_LAUNCH);
     }
     return PV_OK;
 }
@@ -343,23 +348,29 @@ void pv_shutdown(void) {
 
 int pv_set_timing(int enable) {
     g_ctx.timing = enable != 0;
+    g_ctx.ev_used = 0;
     return PV_OK;
 }
 
-int pv_last_kernel_times(double* prep_ms, double* msm_ms) {
-    if (!g_ctx.timing || g_ctx.device < 0 || g_ctx.ev_used == 0)
-        return fail(PV_ERR_ARG, "pv_last_kernel_times: timing disabled or nothing launched");
-    double p = 0, m = 0;
-    for (int c = 0; c < g_ctx.ev_used / 3; c++) {
-        float a = 0, b = 0;
-        PV_HIP(hipEventSynchronize(g_ctx.ev[3 * c + 2]), PV_ERR_LAUNCH);
-        PV_HIP(hipEventElapsedTime(&a, g_ctx.ev[3 * c], g_ctx.ev[3 * c + 1]), PV_ERR_LAUNCH);
-        PV_HIP(hipEventElapsedTime(&b, g_ctx.ev[3 * c + 1], g_ctx.ev[3 * c + 2]), PV_ERR_LAUNCH);
+int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* launches) {
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_kernel_times: call pv_init first");
+    double p = 0, t = 0, m = 0;
+    const int nq = g_ctx.ev_used / 4;
+    for (int c = 0; c < nq; c++) {
+        hipEvent_t* e = &g_ctx.ev[4 * c];
+        float a = 0, b = 0, d = 0;
+        PV_HIP(hipEventSynchronize(e[3]), PV_ERR_LAUNCH);
+        PV_HIP(hipEventElapsedTime(&a, e[0], e[1]), PV_ERR_LAUNCH);
+        PV_HIP(hipEventElapsedTime(&b, e[1], e[2]), PV_ERR_LAUNCH);
+        PV_HIP(hipEventElapsedTime(&d, e[2], e[3]), PV_ERR_LAUNCH);
         p += a;
-        m += b;
+        t += b;
+        m += d;
     }
     if (prep_ms) *prep_ms = p;
+    if (table_ms) *table_ms = t;
     if (msm_ms) *msm_ms = m;
+    if (launches) *launches = nq;
     return PV_OK;
 }
 

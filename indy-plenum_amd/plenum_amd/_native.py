@@ -32,7 +32,8 @@ SIGNATURES = {
     "pv_verify_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "pv_set_timing": (ctypes.c_int, [ctypes.c_int]),
-    "pv_last_kernel_times": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "pv_kernel_times": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "pv_b58decode_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     "pv_b58encode": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]),

@@ -13,7 +13,7 @@
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return 1; } } while (0)
 
 constexpr int NACC = 8;
-constexpr int ITERS = 4096;
+constexpr int ITERS = 65536;
 
 #define BODY_MAD64(i) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc64[i]) : "v"(a[i]), "v"(b) : "vcc");
 #define BODY_MULLO(i) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b));

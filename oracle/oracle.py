@@ -19,6 +19,10 @@ class Oracle:
             build()
         self.lib = ctypes.CDLL(_LIB)
         self.lib.oracle_sign_open.restype = ctypes.c_int
+        self.lib.oracle_sign_open.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+        self.lib.oracle_sign_open_batch.restype = None
+        self.lib.oracle_sign_open_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
 
     def sign_open_ok(self, sm: bytes, pk: bytes) -> bool:
         assert len(pk) == 32

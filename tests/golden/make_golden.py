@@ -1,0 +1,293 @@
+"""Generate the committed golden fixtures by running the REFERENCE itself (/root/reference).
+
+TEST INFRASTRUCTURE, run in the build container only (the reference never ships to the GPU box):
+    python tests/golden/make_golden.py
+The reference's missing third-party modules are provided by tests/golden/_shims: libnacl (ctypes
+over the image's libsodium 1.0.18, the version the reference pins), base58 (oracle/base58_ref.py),
+and stubs for zmq/jsonpickle that the hot path never calls. Outputs (all JSON, data only):
+  serializer.json    serialize_msg_for_signing KATs (incl. the INDY-1469 nested-dict ambiguity)
+  didverifier.json   DidVerifier resolution results / exception class + message
+  authn.json         CoreAuthNr.authenticate / authenticate_multi outcomes on signed requests
+  reqauth.json       ReqAuthenticator.authenticate sequences (cache, query, NoAuthenticatorFound)
+  verdicts.json      libsodium crypto_sign_open verdicts on normal + adversarial (sm, pk) vectors
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = "/root/reference"
+sys.path[:0] = [os.path.join(HERE, "_shims"), REF, ROOT, os.path.join(ROOT, "tests")]
+
+import base58  # noqa: E402  (the shim)
+from common.serializers.serialization import serialize_msg_for_signing  # noqa: E402
+from plenum.common.exceptions import InvalidKey  # noqa: E402,F401
+from plenum.common.request import Request  # noqa: E402
+from plenum.common.signer_did import DidSigner  # noqa: E402
+from plenum.common.signer_simple import SimpleSigner  # noqa: E402
+from plenum.common.verifier import DidVerifier  # noqa: E402
+from plenum.server.client_authn import CoreAuthNr  # noqa: E402
+from plenum.server.req_authenticator import ReqAuthenticator  # noqa: E402
+
+from oracle.libsodium_ref import LibSodium  # noqa: E402
+from oracle.oracle import Oracle  # noqa: E402
+from vectors import VectorGen  # noqa: E402
+
+
+def outcome(fn):
+    try:
+        r = fn()
+        if isinstance(r, set):
+            return {"set": sorted(r)}
+        if isinstance(r, list):
+            return {"list": r}
+        return {"value": r}
+    except Exception as ex:
+        return {"exc": type(ex).__name__, "msg": str(ex)}
+
+
+def dump(name, obj):
+    with open(os.path.join(HERE, name), "w") as f:
+        json.dump(obj, f, indent=1)  # insertion order matters (signature dicts)
+    print("wrote", name, len(obj) if hasattr(obj, "__len__") else "")
+
+
+# ----------------------------------------------------------------------------- serializer
+def gen_serializer():
+    from collections import OrderedDict  # noqa: F401  (literal inputs may use it)
+    inputs = [
+        "1", "'aaa'", "None", "{1: 'a', 2: 'b'}", "{'2': 'b', '1': 'a'}", "[1, 5, 3, 4, 2]",
+        "OrderedDict([('1', 'a'), ('2', 'b')])", "OrderedDict([('2', 'b'), ('1', 'a')])",
+        "{1: 'a', 2: 'b', 3: [1, {2: 'k'}]}", "{'1': 'a', '2': 'b', '3': ['1', {'2': 'k'}]}",
+        "{1: 'a', 2: {3: 'b', 4: {5: {6: 'c'}}}}", "{1: 'a', 2: {3: 'b'}, 4: {5: {6: 'c'}}}",
+        "{'1': 'a', '2': 'b', '3': {'4': 'c', '5': 'd', '6': {'7': {'8': 'e', '9': 'f'}, "
+        "'10': {'11': 'g', '12': 'h'}}, '13': {'13': {'13': 'i'}}}}",
+        "OrderedDict([('2', OrderedDict([('4', 'c'), ('3', 'b')])), ('1', 'a')])",
+        "{'a': True, 'b': False, 'c': 1.5, 'd': None, 'e': [], 'f': {}, 'g': [None, 2.25, 'x']}",
+        "{'identifier': 'V4SGRU86Z58d6TV7PBUe6f', 'reqId': 1700000000000001, 'protocolVersion': 2, "
+        "'operation': {'type': '1', 'dest': 'V4SGRU86Z58d6TV7PBUe6f', 'verkey': '~CoRER63DVYnWZtK8uAzNbx', "
+        "'alias': 'u00000001'}, 'taaAcceptance': {'taaDigest': '" + "ab" * 32 + "', "
+        "'mechanism': 'service_agreement', 'time': 1700000000}}",
+        "{'x': 'ünïcödé', 'y': ['€', 1e100, -0.0, 10**30]}",
+        "{'signature': 'S', 'signatures': {'a': 'b'}, 'fees': [1], 'k': 'v'}",
+        "(1, 2)", "b'bytes'", "{'k': (1, 2)}", "{1: 'a', '2': 'b'}",
+    ]
+    ignore_sets = [None, ["signature"], ["signature", "signatures", "fees"]]
+    out = []
+    for src in inputs:
+        for ign in ignore_sets:
+            obj = eval(src)  # literal fixtures defined above
+            res = outcome(lambda: serialize_msg_for_signing(obj, topLevelKeysToIgnore=ign).hex())
+            out.append({"input": src, "ignore": ign, "out": res})
+    return out
+
+
+# ----------------------------------------------------------------------------- DidVerifier
+def gen_didverifier():
+    cases = [("~8zH9ZSyZTFPGJ4ZPL5Rvxx", "99BgFBg35BehzfSADV5nM4"),  # test_verifier.py KAT
+             (None, "99BgFBg35BehzfSADV5nM4"), ("", "99BgFBg35BehzfSADV5nM4"),
+             ("FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFF", None),  # odd-length verkey KAT
+             ("5SMfqc4NGeQM21NMx3cB9sqop6KCFFC1TqoGKGptdock", None),
+             ("5SMfqc4NGeQM21NMx3cB9sqop6KCFFC1TqoGKGptdock", "99BgFBg35BehzfSADV5nM4"),
+             (None, None), ("", None), ("~", "99BgFBg35BehzfSADV5nM4"), ("~0OIl", "99BgFBg35BehzfSADV5nM4"),
+             ("~8zH9ZSyZTFPGJ4ZPL5Rvxx", "0OIl"), ("~8zH9ZSyZTFPGJ4ZPL5Rvxx", None),
+             ("~8zH9ZSyZTFPGJ4ZPL5Rvxx", "   "), ("5SMfqc4NGeQM21NMx3cB9sqop6KCFFC1TqoGKGptdock  ", None),
+             ("5SMfqc4NGeQM21NMx3cB9sqop6KCFFC1TqoGKGptdoc", None), ("11111111111111111111111111111111", None),
+             ("1111111111111111111111111111111111", None)]
+    # cryptonyms (identifier = full b58 verkey) and DidSigner pairs
+    for i in range(6):
+        s = DidSigner(seed=bytes([65 + i]) * 32)
+        cases.append((s.verkey, s.identifier))
+        ss = SimpleSigner(seed=bytes([97 + i]) * 32)
+        cases.append((None, ss.identifier))
+        cases.append(("", ss.identifier))
+        cases.append((ss.verkey, None))
+    # hex-encoded verkey: b58(hex string of a 32-byte key) goes through VerifyKey(key, HexEncoder)
+    hexkey = base58.b58encode(b"ab" * 32).decode()
+    cases += [(hexkey, None), (base58.b58encode(b"ab" * 31 + b"zz").decode(), None),
+              (base58.b58encode(b"abc").decode(), None)]
+    out = []
+    for vk, idr in cases:
+        def run():
+            v = DidVerifier(vk, identifier=idr)
+            key = v._vr.key
+            return {"verkey": v.verkey, "raw": bytes(key).hex() if key else None}
+        out.append({"verkey": vk, "identifier": idr, "out": outcome(run)})
+    return out
+
+
+# ----------------------------------------------------------------------------- authn
+class RefState:
+    """state.get(key, isCommitted) over {sha256(nym): json} (request_handlers/utils.py:30-39)."""
+
+    def __init__(self, nyms):
+        from hashlib import sha256
+        self.kv = {sha256(n.encode()).digest(): json.dumps(r).encode() for n, r in nyms.items()}
+
+    def get(self, key, isCommitted=True):
+        return self.kv.get(key)
+
+
+def nym_op(signer, i):
+    return {"type": "1", "dest": signer.identifier, "verkey": signer.verkey, "alias": "u%08d" % i}
+
+
+def signed_request(signer, i, extra=None, op=None):
+    req = Request(identifier=signer.identifier, reqId=1700000000000000 + i, operation=op or nym_op(signer, i),
+                  protocolVersion=2)
+    if extra:
+        for k, v in extra.items():
+            setattr(req, k, v)
+    req.signature = signer.sign(req.signingPayloadState())
+    return req.as_dict
+
+
+def multi_signed(signers, i, bad=()):
+    req = Request(identifier=signers[0].identifier, reqId=1700000000100000 + i,
+                  operation={"type": "101", "x": i}, protocolVersion=2)
+    sigs = {}
+    for j, s in enumerate(signers):
+        sig = s.sign(req.signingPayloadState())
+        if j in bad:
+            raw = bytearray(base58.b58decode(sig))
+            raw[5] ^= 1
+            sig = base58.b58encode(bytes(raw)).decode()
+        sigs[s.identifier] = sig
+    d = req.as_dict
+    d["signatures"] = sigs
+    return d
+
+
+def gen_authn():
+    signers = [DidSigner(seed=("signer%026d" % i).encode()) for i in range(5)]
+    crypt = SimpleSigner(seed=b"c" * 32)
+    unregistered = DidSigner(seed=b"u" * 32)
+    clients = {s.identifier: s.verkey for s in signers[:4]}
+    clients[crypt.identifier] = ""  # cryptonym: DidVerifier uses the identifier itself
+    clients[signers[4].identifier] = base58.b58encode(base58.b58decode(signers[4].identifier) + base58.b58decode(
+        signers[4].verkey[1:])).decode()  # full (non-abbreviated) verkey
+    state_nyms = {unregistered.identifier: {"verkey": unregistered.verkey, "role": None}}
+    cases = []
+
+    def add(kind, req, **kw):
+        cases.append({"kind": kind, "req": req, "kw": kw})
+
+    for i, s in enumerate(signers + [crypt]):
+        add("authenticate", signed_request(s, i))
+    add("authenticate", signed_request(unregistered, 10))  # verkey from uncommitted state
+    fresh = DidSigner(seed=b"f" * 32)
+    add("authenticate", signed_request(fresh, 11))  # NYM dest == identifier: self verkey
+    fresh2 = DidSigner(seed=b"g" * 32)
+    r = signed_request(fresh2, 12, op={"type": "101", "dest": fresh2.identifier})
+    add("authenticate", r)  # not NYM, unknown DID -> CouldNotAuthenticate
+    r = signed_request(signers[0], 13)
+    r["reqId"] += 1
+    add("authenticate", r)  # tampered -> InsufficientCorrectSignatures
+    r = signed_request(signers[0], 14)
+    r["identifier"] = signers[1].identifier
+    add("authenticate", r)  # wrong key
+    r = signed_request(signers[0], 15)
+    r["signature"] = "0OIl" + r["signature"][4:]
+    add("authenticate", r)  # invalid base58 -> InvalidSignatureFormat
+    r = signed_request(signers[0], 16)
+    raw = base58.b58decode(r["signature"])
+    r2 = dict(r, signature=base58.b58encode(raw[:63]).decode())
+    add("authenticate", r2)  # 63-byte signature: sm split point shifts
+    r3 = dict(r, signature=base58.b58encode(raw + b"\x00").decode())
+    add("authenticate", r3)  # 65 bytes
+    r4 = dict(r, signature=base58.b58encode(raw[:10]).decode())
+    add("authenticate", r4)
+    r = signed_request(signers[0], 17)
+    del r["signature"]
+    add("authenticate", r)  # MissingSignature
+    r = signed_request(signers[0], 18)
+    r["signature"] = ""
+    add("authenticate", r)  # empty signature with identifier -> signatures None -> TypeError
+    r = signed_request(signers[0], 19)
+    r["fees"] = [["utxo", 1]]
+    add("authenticate", r)  # fees excluded from signing
+    r = signed_request(signers[0], 20)
+    r["signature"] = r["signature"] + "  "
+    add("authenticate", r)  # trailing whitespace stripped by b58decode
+    r = signed_request(signers[0], 21)
+    del r["identifier"]
+    add("authenticate", r)  # signature without identifier -> signatures None
+    r = signed_request(signers[0], 22)
+    add("authenticate", r, identifier=signers[0].identifier, signature=r["signature"])
+    ms = signers[:3]
+    for bad in [(), (0,), (1,), (2,), (0, 2), (0, 1, 2)]:
+        d = multi_signed(ms, 30 + len(cases), bad)
+        add("authenticate", d)
+        for th in (None, 1, 2, 3, 4):
+            payload = {k: v for k, v in d.items() if k not in ("signature", "signatures", "fees")}
+            add("authenticate_multi", payload, signatures=d["signatures"], threshold=th)
+    d = multi_signed(ms, 50)
+    d["signatures"] = {}
+    add("authenticate", d)
+    d = multi_signed(ms + [unregistered], 51)
+    add("authenticate", d)  # 4th signer resolved from state
+    d = multi_signed(ms + [DidSigner(seed=b"h" * 32)], 52)
+    add("authenticate", d)  # unknown co-signer -> CouldNotAuthenticate (after 3 good ones)
+    d = multi_signed(ms, 53)
+    d["signatures"][signers[1].identifier] = "invalid!!"
+    add("authenticate", d)  # invalid base58 in position 2
+    out = []
+    for c in cases:
+        authnr = CoreAuthNr(["1", "101"], ["105"], ["action"], state=RefState(state_nyms))
+        for idr, vk in clients.items():
+            authnr.addIdr(idr, vk)
+        if c["kind"] == "authenticate":
+            res = outcome(lambda: authnr.authenticate(json.loads(json.dumps(c["req"])), **c["kw"]))
+        else:
+            res = outcome(lambda: authnr.authenticate_multi(json.loads(json.dumps(c["req"])), **c["kw"]))
+        out.append(dict(c, out=res))
+    return {"clients": clients, "state_nyms": state_nyms, "cases": out}
+
+
+def gen_reqauth():
+    signers = [DidSigner(seed=("rasigner%024d" % i).encode()) for i in range(3)]
+    clients = {s.identifier: s.verkey for s in signers}
+    seqs = []
+    good = signed_request(signers[0], 1)
+    bad = dict(good, reqId=good["reqId"] + 1)
+    other = signed_request(signers[1], 2)
+    query = signed_request(signers[2], 3, op={"type": "105", "dest": signers[2].identifier})
+    unknown_type = signed_request(signers[2], 4, op={"type": "999"})
+    resigned = signed_request(signers[0], 1)  # same digest key, same signature
+    alt_sig = dict(good, signature=other["signature"])  # same key, different signature
+    seqs.append([(good, "k1"), (good, "k1"), (bad, "k2"), (other, "k3"), (query, "k4"), (unknown_type, "k5"),
+                 (resigned, "k1"), (alt_sig, "k1"), (good, None), (bad, None)])
+    seqs.append([(bad, "kb"), (bad, "kb"), (good, "kb"), (bad, "kb")])
+    out = []
+    for seq in seqs:
+        ra = ReqAuthenticator()
+        core = CoreAuthNr(["1", "101"], ["105"], ["action"], state=RefState({}))
+        for idr, vk in clients.items():
+            core.addIdr(idr, vk)
+        ra.register_authenticator(core)
+        res = [outcome(lambda: ra.authenticate(json.loads(json.dumps(req)), key)) for req, key in seq]
+        out.append({"items": [[req, key] for req, key in seq], "out": res})
+    # no authenticator registered / core_authenticator error
+    ra = ReqAuthenticator()
+    out.append({"items": [[good, "k"]], "out": [outcome(lambda: ra.authenticate(good, "k"))]})
+    return {"clients": clients, "seqs": out}
+
+
+def gen_verdicts():
+    ls, o = LibSodium(), Oracle()
+    g = VectorGen(ls, o, seed=2024)
+    out = []
+    for cls in VectorGen.CLASSES:
+        for _ in range(12 if cls != "mixed_order_A" else 40):
+            sm, pk = g.make(cls)
+            out.append({"cls": cls, "sm": sm.hex(), "pk": pk.hex(), "ok": ls.sign_open_ok(sm, pk)})
+    return out
+
+
+if __name__ == "__main__":
+    dump("serializer.json", gen_serializer())
+    dump("didverifier.json", gen_didverifier())
+    dump("authn.json", gen_authn())
+    dump("reqauth.json", gen_reqauth())
+    dump("verdicts.json", gen_verdicts())

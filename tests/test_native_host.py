@@ -1,0 +1,158 @@
+"""The kernels' own arithmetic (indy-plenum_amd/csrc/*.h), compiled for the HOST with bound
+assertions enabled (tests/native/hostcheck.hip), against Python big integers, the oracle, the
+golden libsodium verdicts and libsodium itself. Same source as the GPU code, so a pass here means
+the GPU arithmetic is right up to compilation; tests/test_gpu_parity.py closes that gap."""
+import ctypes
+import json
+import os
+import random
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "native", "libhostcheck.so")
+P = 2 ** 255 - 19
+L = 2 ** 252 + 27742317777372353535851937790883648493
+W = [26 if i % 2 == 0 else 25 for i in range(10)]
+A10 = ctypes.c_uint32 * 10
+
+
+def build_hostcheck():
+    src = os.path.join(HERE, "native", "hostcheck.hip")
+    cmd = ["/opt/rocm/bin/hipcc", "-O2", "-fPIC", "-shared", "--offload-arch=gfx950", "--offload-host-only",
+           "-I" + os.path.join(ROOT, "indy-plenum_amd", "csrc"), src, "-o", LIB]
+    subprocess.check_call(cmd)
+
+
+@pytest.fixture(scope="module")
+def hc():
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
+            os.path.getmtime(os.path.join(ROOT, "indy-plenum_amd", "csrc", f))
+            for f in os.listdir(os.path.join(ROOT, "indy-plenum_amd", "csrc")) if f.endswith(".h")):
+        build_hostcheck()
+    return ctypes.CDLL(LIB)
+
+
+def to_limbs(x):
+    out, off = [], 0
+    for w in W:
+        out.append((x >> off) & ((1 << w) - 1))
+        off += w
+    return out
+
+
+def from_limbs(lim):
+    v, off = 0, 0
+    for i, w in enumerate(W):
+        v += lim[i] << off
+        off += w
+    return v
+
+
+def max_mul_input():
+    return [3 * (1 << w) + (1 << 18) - 1 for w in W]
+
+
+def test_fe_mul_sq_random_and_extreme(hc):
+    rng = random.Random(7)
+    cases = [(max_mul_input(), max_mul_input())]
+    for _ in range(3000):
+        f = [rng.randrange(3 * (1 << w) + (1 << 18)) for w in W]
+        g = [rng.randrange(3 * (1 << w) + (1 << 18)) for w in W]
+        cases.append((f, g))
+        cases.append((to_limbs(rng.randrange(P)), to_limbs(rng.randrange(P))))
+    h = A10()
+    for f, g in cases:
+        hc.hc_fe_mul(h, A10(*f), A10(*g))
+        assert from_limbs(list(h)) % P == from_limbs(f) * from_limbs(g) % P
+        hc.hc_fe_sq(h, A10(*f))
+        assert from_limbs(list(h)) % P == from_limbs(f) ** 2 % P
+
+
+def test_fe_tobytes_canonical_edges(hc):
+    s = ctypes.create_string_buffer(32)
+    for v in [0, 1, 18, 19, P - 1, P, P + 1, P + 18, 2 ** 255 - 1]:
+        hc.hc_fe_tobytes(s, A10(*to_limbs(v)))
+        assert int.from_bytes(s.raw, "little") == v % P, v
+    for v in [P, 2 * P - 1, 2 * P, 2 * P + 7, 3 * P]:  # non-normalised representations
+        lim = to_limbs(v % 2 ** 255)
+        lim[0] += v - from_limbs(lim)
+        if lim[0] < 2 ** 31:
+            hc.hc_fe_tobytes(s, A10(*lim))
+            assert int.from_bytes(s.raw, "little") == v % P, v
+
+
+def test_fe_invert_pow(hc):
+    rng = random.Random(8)
+    h = A10()
+    for _ in range(40):
+        x = rng.randrange(1, P)
+        hc.hc_fe_invert(h, A10(*to_limbs(x)))
+        assert from_limbs(list(h)) * x % P == 1
+        hc.hc_fe_pow22523(h, A10(*to_limbs(x)))
+        assert from_limbs(list(h)) % P == pow(x, (P - 5) // 8, P)
+
+
+def test_scalar_reduce_canonical_recode(hc):
+    rng = random.Random(9)
+    r = ctypes.create_string_buffer(32)
+    edges = [0, 2 ** 512 - 1, L, L - 1, L + 1, 2 ** 256, 2 ** 252, 2 * L, L * 2 ** 259, 2 ** 511]
+    for x in edges + [rng.getrandbits(512) for _ in range(5000)]:
+        hc.hc_sc_reduce64(r, x.to_bytes(64, "little"))
+        assert int.from_bytes(r.raw, "little") == x % L
+    for s in [L, L - 1, L + 1, 0, 2 ** 256 - 1, 2 ** 253] + [rng.getrandbits(256) for _ in range(2000)]:
+        assert hc.hc_sc_is_canonical(s.to_bytes(32, "little")) == (s < L)
+    for a in [0, 1, L - 1, 2 ** 252] + [rng.randrange(L) for _ in range(2000)]:
+        hc.hc_sc_recode16(r, a.to_bytes(32, "little"))
+        nib = [(r.raw[i // 2] >> (4 * (i % 2))) & 15 for i in range(64)]
+        assert sum((n - 16 if n >= 8 else n) * 16 ** i for i, n in enumerate(nib)) == a
+        assert all(-8 <= (n - 16 if n >= 8 else n) <= 8 for n in nib)
+        hc.hc_sc_recode256(r, a.to_bytes(32, "little"))
+        assert sum((b - 256 if b >= 128 else b) * 256 ** i for i, b in enumerate(r.raw)) == a
+
+
+def test_small_order_and_canonical_rules(hc):
+    from vectors import BLACKLIST
+    for b in BLACKLIST:
+        for top in (0, 0x80):
+            e = bytearray(b)
+            e[31] |= top
+            assert hc.hc_has_small_order(bytes(e)) == 1
+    assert hc.hc_has_small_order(bytes([2]) + bytes(31)) == 0
+    for y in range(P - 3, 2 ** 255):
+        assert hc.hc_ge_is_canonical(y.to_bytes(32, "little")) == (y < P)
+
+
+def test_base_point_table(hc, oracle):
+    tab = (ctypes.c_uint32 * (129 * 32))()
+    hc.hc_build_b_table(tab)
+    d = (-121665 * pow(121666, P - 2, P)) % P
+    for j in [0, 1, 2, 3, 64, 127, 128]:
+        e = tab[j * 32:(j + 1) * 32]
+        ypx, ymx, xy2d = from_limbs(e[0:10]), from_limbs(e[10:20]), from_limbs(e[20:30])
+        y = (ypx + ymx) * pow(2, P - 2, P) % P
+        x = (ypx - ymx) * pow(2, P - 2, P) % P
+        assert xy2d == 2 * d * x * y % P
+        enc = bytearray(y.to_bytes(32, "little"))
+        enc[31] |= (x & 1) << 7
+        want = oracle.scalarmult_base(j.to_bytes(32, "little")) if j else (1).to_bytes(32, "little")
+        assert bytes(enc) == want, j
+
+
+def test_pipeline_matches_golden_verdicts(hc):
+    with open(os.path.join(HERE, "golden", "verdicts.json")) as f:
+        cases = json.load(f)
+    for c in cases:
+        sm, pk = bytes.fromhex(c["sm"]), bytes.fromhex(c["pk"])
+        assert bool(hc.hc_sign_open(sm, ctypes.c_uint64(len(sm)), pk)) == c["ok"], c["cls"]
+
+
+def test_pipeline_vs_libsodium(hc, sodium, oracle):
+    from vectors import VectorGen
+    g = VectorGen(sodium, oracle, seed=21)
+    for cls in VectorGen.CLASSES:
+        for _ in range(10):
+            sm, pk = g.make(cls)
+            assert bool(hc.hc_sign_open(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls

@@ -1,0 +1,138 @@
+"""Synthetic NYM-style signed requests for bench.py and the large GPU tests.
+
+Template (signing-serialized with the reference's rules: sorted keys, "k:v" joined by "|"):
+  {identifier: DID_s, reqId: 1700000000000000 + i, protocolVersion: 2,
+   operation: {type: '1', dest: DID_i, verkey: '~' + b58(16 B), alias: 'u%08d' % i},
+   taaAcceptance: {taaDigest: 64 hex, mechanism: 'service_agreement', time: 1700000000}}
+The signer pool has 1024 DidSigner-style identities: seed_s = SHA-512("plenum-bench" || u64 s)[:32],
+vk = Ed25519 public key, DID = b58(vk[:16]), abbreviated verkey = '~' + b58(vk[16:]).
+Messages are rendered directly in signing-serialized form (checked against
+plenum_amd.serialization.serialize_msg_for_signing on a sample), then signed with the image's
+libsodium (crypto_sign_detached) in worker processes. Everything is seeded and deterministic.
+"""
+import ctypes
+import hashlib
+import multiprocessing as mp
+import os
+import struct
+
+import numpy as np
+
+B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
+POOL = 1024
+TAA_DIGEST = hashlib.sha256(b"plenum-bench-taa").hexdigest()
+_SODIUM = None
+
+
+def b58(data: bytes) -> str:
+    n0 = len(data) - len(data.lstrip(b"\0"))
+    v = int.from_bytes(data, "big")
+    out = ""
+    while v:
+        v, r = divmod(v, 58)
+        out = B58[r] + out
+    return "1" * n0 + out
+
+
+def sodium():
+    global _SODIUM
+    if _SODIUM is None:
+        for p in ("/opt/conda/lib/libsodium.so.23", "/usr/lib/x86_64-linux-gnu/libsodium.so.23"):
+            if os.path.exists(p):
+                lib = ctypes.CDLL(p)
+                lib.sodium_init()
+                _SODIUM = lib
+                break
+        else:
+            raise OSError("libsodium.so.23 is needed to sign the synthetic workload")
+    return _SODIUM
+
+
+def signer(s):
+    seed = hashlib.sha512(b"plenum-bench" + struct.pack("<Q", s)).digest()[:32]
+    pk = ctypes.create_string_buffer(32)
+    sk = ctypes.create_string_buffer(64)
+    sodium().crypto_sign_seed_keypair(pk, sk, seed)
+    vk = pk.raw
+    return {"sk": sk.raw, "vk": vk, "did": b58(vk[:16]), "abbr": "~" + b58(vk[16:])}
+
+
+def request_dict(i, s):
+    h = hashlib.sha256(struct.pack("<Q", i)).digest()
+    return {
+        "identifier": s["did"], "reqId": 1700000000000000 + i, "protocolVersion": 2,
+        "operation": {"type": "1", "dest": b58(h[:16]), "verkey": "~" + b58(h[16:]), "alias": "u%08d" % i},
+        "taaAcceptance": {"taaDigest": TAA_DIGEST, "mechanism": "service_agreement", "time": 1700000000},
+    }
+
+
+def message(i, s):
+    """serialize_msg_for_signing(request_dict(i, s)) rendered directly."""
+    h = hashlib.sha256(struct.pack("<Q", i)).digest()
+    return ("identifier:%s|operation:alias:u%08d|dest:%s|type:1|verkey:~%s|protocolVersion:2|reqId:%d|"
+            "taaAcceptance:mechanism:service_agreement|taaDigest:%s|time:1700000000"
+            % (s["did"], i, b58(h[:16]), b58(h[16:]), 1700000000000000 + i, TAA_DIGEST)).encode()
+
+
+_POOL_CACHE = None
+
+
+def _pool():
+    global _POOL_CACHE
+    if _POOL_CACHE is None:
+        _POOL_CACHE = [signer(s) for s in range(POOL)]
+    return _POOL_CACHE
+
+
+def _sign_range(args):
+    lo, hi = args
+    pool = _pool()
+    lib = sodium()
+    sig = ctypes.create_string_buffer(64)
+    out_sm, out_pk = [], []
+    for i in range(lo, hi):
+        s = pool[i % POOL]
+        m = message(i, s)
+        lib.crypto_sign_detached(sig, None, m, ctypes.c_ulonglong(len(m)), s["sk"])
+        out_sm.append(sig.raw + m)
+        out_pk.append(s["vk"])
+    return b"".join(out_sm), [len(x) for x in out_sm], b"".join(out_pk)
+
+
+def generate(lo, n, workers=None):
+    """Requests [lo, lo + n): (blob uint8, offsets uint64[n+1], pks uint8[n, 32])."""
+    workers = workers or min(16, max(1, (os.cpu_count() or 1)))
+    chunk = max(1, (n + workers * 4 - 1) // (workers * 4))
+    ranges = [(a, min(a + chunk, lo + n)) for a in range(lo, lo + n, chunk)]
+    if workers > 1 and n > 20000:
+        ctx = mp.get_context("fork")
+        with ctx.Pool(workers) as p:
+            parts = p.map(_sign_range, ranges)
+    else:
+        parts = [_sign_range(r) for r in ranges]
+    blob = np.frombuffer(b"".join(p[0] for p in parts), dtype=np.uint8)
+    lens = np.array([x for p in parts for x in p[1]], dtype=np.uint64)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    pks = np.frombuffer(b"".join(p[2] for p in parts), dtype=np.uint8).reshape(n, 32)
+    return blob, off, pks
+
+
+def save(path, lo, n, workers=None):
+    blob, off, pks = generate(lo, n, workers)
+    np.savez(path, blob=blob, off=off, pks=pks, lo=np.array([lo]))
+
+
+def load(path):
+    d = np.load(path, allow_pickle=False)
+    return d["blob"], d["off"], d["pks"], int(d["lo"][0])
+
+
+if __name__ == "__main__":
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--lo", type=int, default=0)
+    a = ap.parse_args()
+    save(a.out, a.lo, a.n)
