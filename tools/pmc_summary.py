@@ -2,7 +2,8 @@
 the roofline uses. Usage: python tools/pmc_summary.py OUT.json DIR [DIR ...] [--requests N]
 
 Derived (MI355X_MICROARCH.md §HBM / rocprofv3 notes):
-  hbm_read_bytes  = FETCH_SIZE(KiB) * 1024 * 2   (gfx950 FETCH_SIZE reports half of wide coalesced reads)
+  hbm_read_bytes  = FETCH_SIZE(KiB) * 1024        (raw; the gfx950 x2 correction is calibrated only for
+                    wide coalesced streaming reads, so the corrected figure is kept as an upper bound)
   hbm_write_bytes = WRITE_SIZE(KiB) * 1024
   eff_clock_GHz   = GRBM_GUI_ACTIVE / 8 XCDs / kernel seconds
   valu_lane_instr_per_request = SQ_INSTS_VALU * 64 / requests
@@ -47,7 +48,8 @@ def main():
         secs = sorted(dur[k])[len(dur[k]) // 2]
         d = {"counters_per_dispatch": avg, "median_dispatch_s_under_pmc": secs}
         if "FETCH_SIZE" in avg:
-            d["hbm_read_bytes"] = avg["FETCH_SIZE"] * 1024 * 2
+            d["hbm_read_bytes"] = avg["FETCH_SIZE"] * 1024
+            d["hbm_read_bytes_x2_upper"] = avg["FETCH_SIZE"] * 1024 * 2
         if "WRITE_SIZE" in avg:
             d["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
         if "hbm_read_bytes" in d and "hbm_write_bytes" in d:
