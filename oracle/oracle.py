@@ -65,3 +65,26 @@ class Oracle:
         self.lib.oracle_sha512_3(out, data, ctypes.c_size_t(len(data)), None, ctypes.c_size_t(0), None,
                                  ctypes.c_size_t(0))
         return out.raw
+
+
+def cpu_verdicts(blob, off, pks, threads=None):
+    """Per-record crypto_sign_open verdicts from libsodium 1.0.18 (the oracle if it is absent), threaded."""
+    import numpy as np
+    from oracle.libsodium_ref import find_libsodium
+    o = Oracle()
+    fn = o.lib.cpu_verdicts
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+    path = find_libsodium()
+    threads = threads or min(16, len(os.sched_getaffinity(0)))
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    pks = np.ascontiguousarray(pks, dtype=np.uint8)
+    n = len(off) - 1
+    out = np.zeros(n, dtype=np.uint8)
+    rc = fn((path or "").encode(), 1 if path else 0, blob.ctypes.data, off.ctypes.data, pks.ctypes.data, n, threads,
+            out.ctypes.data)
+    if rc != 0:
+        raise OSError("cpu_verdicts failed")
+    return out.astype(bool)
