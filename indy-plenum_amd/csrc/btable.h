@@ -62,6 +62,11 @@ inline void pv_build_b_table(uint32_t* out /* PV_BTAB_ENTRIES * PV_BTAB_STRIDE *
 // Host/LDS-agnostic reader of the flat table.
 struct pv_btab_flat {
     const uint32_t* base;
+    // part 0: words 0..19 (y+x, y-x); part 1: words 20..29 (2d x y) into w[0..9]
+    PV_HD void load_part(int j, int part, uint32_t w[20]) const {
+        const uint32_t* e = base + j * PV_BTAB_STRIDE + 20 * part;
+        for (int i = 0; i < (part ? 10 : 20); i++) w[i] = e[i];
+    }
     PV_HD void load(int j, ge_niels& q) const {
         const uint32_t* e = base + j * PV_BTAB_STRIDE;
 #pragma unroll

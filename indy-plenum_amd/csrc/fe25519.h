@@ -2,19 +2,26 @@
 //
 // Representation: 10 unsigned 32-bit limbs in radix 2^25.5 (limb i has weight 2^ceil(25.5 i):
 // even limbs carry 26 bits, odd limbs 25 bits). Products are formed with v_mad_u64_u32
-// (32x32 -> 64 multiply + 64-bit accumulate in one instruction). Measured on MI355X it issues at
-// ~5.2 cycles per wave64 instruction at >= 2 waves/SIMD, the same rate as a bare v_mul_lo_u32
-// (profiles/r01_isa_rates.jsonl), so one mad replaces mul_lo + mul_hi + add_co + addc. 5x51-bit
-// limbs would need 64x64 -> 128 products that the VALU does not have.
+// (32x32 -> 64 multiply + 64-bit accumulate in one instruction, 4 cycles per wave64 instruction
+// on gfx950 - profiles/r01_isa_rates_full.jsonl). 5x51-bit limbs would need 64x64 -> 128 products
+// that the VALU does not have.
 //
-// Bound discipline (checked by tests/test_native_host.py with the PV_BOUNDS_CHECK host build):
-//   "R"   reduced:     limb < 2^width + 2^17 (width 26 even / 25 odd; output of mul/sq/carry:
-//                      the carries into limbs 1 and 5 are not re-propagated)
-//   mul/sq inputs:     limb < 3 * 2^width + 2^18
-//                      => 19 * limb < 2^32 and every product column < 2^63 (no 64-bit overflow)
-//   fe_add(R, R)  -> even < 2^27, odd < 2^26          (valid mul input)
-//   fe_sub(X, R)  -> X + 2p - R: needs X in R           (valid mul input)
-//   anything else  -> fe_carry first.
+// Multiplication is PRODUCT-SCANNING: column k of the (19-folded) schoolbook product is one
+// v_mad_u64_u32 chain whose accumulator starts at the carry out of column k-1, so carrying costs
+// one v_lshrrev_b64 + one v_and_b32 per limb and no separate 64-bit adds. The wrapped products
+// use 19*g (computed once per operand by the caller when it is shared, fe_mul_pre) and odd x odd
+// products use 2*f. On the device every multiply-accumulate is an explicit v_mad_u64_u32 (inline
+// asm): left to itself the compiler widens a 32-bit operand whose top bit it cannot bound into a
+// 64 x 32 product (an extra mad + moves per term).
+//
+// Bound discipline (asserted by the PV_BOUNDS_CHECK host build, tests/test_native_host.py):
+//   "R" reduced: limb < 2^width + 2^17. Output of fe_mul / fe_sq / fe_carry.
+//   fe_mul(h, f, g): g limbs < PV_GMAX (19 g < 2^32); f limbs < 2^31; every column < 2^64
+//                    (checked exactly in the host build; all terms are non-negative, so max-limb
+//                    inputs are the worst case and the tests feed them).
+//   fe_sq(h, f):     f limbs < PV_GMAX.
+//   fe_add / fe_sub / fe_sub4p: plain limb arithmetic, see each function.
+//   fe_carry:        any limbs < 2^32 -> R.
 // This file replaces libsodium's fe25519 (ref10, radix 2^25.5 signed limbs), which the reference
 // reaches via stp_core/crypto/nacl_wrappers.py:108 -> libnacl.crypto_sign_open.
 #pragma once
@@ -37,13 +44,14 @@ struct fe {
 
 static constexpr uint32_t M26 = (1u << 26) - 1;
 static constexpr uint32_t M25 = (1u << 25) - 1;
+// largest limb a 19-multiplied operand may have: 19 * PV_GMAX < 2^32
+static constexpr uint32_t PV_GMAX = 0xD000000u;
 
-PV_HD void fe_check_mul_input(const fe& f) {
+PV_HD void fe_check_g(const fe& g) {
 #ifdef PV_BOUNDS_CHECK
-    for (int i = 0; i < 10; i++)
-        PV_ASSERT(f.v[i] < ((i & 1) ? 3u * (1u << 25) : 3u * (1u << 26)) + (1u << 18), "mul input");
+    for (int i = 0; i < 10; i++) PV_ASSERT(g.v[i] < PV_GMAX, "mul g operand");
 #else
-    (void)f;
+    (void)g;
 #endif
 }
 PV_HD void fe_check_reduced(const fe& f) {
@@ -55,6 +63,40 @@ PV_HD void fe_check_reduced(const fe& f) {
 #endif
 }
 
+// ------------------------------------------------------------------ VALU primitives
+// acc + a*b (64-bit) and a*b: one v_mad_u64_u32 each on the device.
+PV_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
+PV_HD uint64_t mul64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+// Opaque copy: stops the compiler from re-associating a column sum so that the carry from the
+// previous column is added by a separate v_lshl_add_u64 instead of entering the first
+// v_mad_u64_u32 of the column as its accumulator (no instruction is emitted).
+PV_HD uint64_t pv_opaque64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(x));
+#endif
+    return x;
+}
+// 2x as a VOP2 add (2 cycles per wave64 instruction) rather than the VOP3-rate shift the compiler
+// picks for x << 1.
+PV_HD uint32_t dbl32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
+    return x + x;
+#endif
+}
+
+// Keeps the machine scheduler from interleaving too many independent field multiplications past
+// the VGPR budget (each one has 55-100 mads, ample ILP at 3 waves/SIMD).
+PV_HD void pv_sched_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+// ------------------------------------------------------------------ limb helpers
 PV_HD void fe_0(fe& h) {
 #pragma unroll
     for (int i = 0; i < 10; i++) h.v[i] = 0;
@@ -71,21 +113,23 @@ PV_HD void fe_add(fe& h, const fe& f, const fe& g) {
 #pragma unroll
     for (int i = 0; i < 10; i++) h.v[i] = f.v[i] + g.v[i];
 }
-// h = f + 2p - g, g reduced
+// h = f + 2p - g, g reduced (R)
 PV_HD void fe_sub(fe& h, const fe& f, const fe& g) {
     fe_check_reduced(g);
     h.v[0] = f.v[0] + 0x7FFFFDAu - g.v[0];
 #pragma unroll
     for (int i = 1; i < 10; i++) h.v[i] = f.v[i] + ((i & 1) ? 0x3FFFFFEu : 0x7FFFFFEu) - g.v[i];
 }
-// h = 4p - g for g with even limbs < 2^28, odd < 2^27 (negation of a non-reduced value);
-// the result is NOT a valid mul input until carried.
+// h = f + 4p - g for g with even limbs < 2^28, odd < 2^27 (e.g. a sum of two R values).
 PV_HD void fe_sub4p(fe& h, const fe& f, const fe& g) {
+#ifdef PV_BOUNDS_CHECK
+    for (int i = 0; i < 10; i++) PV_ASSERT(g.v[i] <= ((i & 1) ? 0x7FFFFFCu : 0xFFFFFB4u), "sub4p operand");
+#endif
     h.v[0] = f.v[0] + 0xFFFFFB4u - g.v[0];
 #pragma unroll
     for (int i = 1; i < 10; i++) h.v[i] = f.v[i] + ((i & 1) ? 0x7FFFFFCu : 0xFFFFFFCu) - g.v[i];
 }
-// conditional negate of a reduced value: h = neg ? 2p - f : f (result < 2^27 even, valid mul input)
+// conditional negate of a reduced value: h = neg ? 2p - f : f (result < 2^27 even, valid g operand)
 PV_HD void fe_cneg(fe& h, const fe& f, bool neg) {
     fe n, z;
     fe_0(z);
@@ -98,118 +142,139 @@ PV_HD void fe_cmov(fe& h, const fe& f, bool c) {
     for (int i = 0; i < 10; i++) h.v[i] = c ? f.v[i] : h.v[i];
 }
 
-// Carry chain over 64-bit column sums (each < 2^63) -> reduced limbs.
-PV_HD void fe_carry64(fe& h, uint64_t t[10]) {
-    t[1] += t[0] >> 26; t[0] &= M26;
-    t[5] += t[4] >> 26; t[4] &= M26;
-    t[2] += t[1] >> 25; t[1] &= M25;
-    t[6] += t[5] >> 25; t[5] &= M25;
-    t[3] += t[2] >> 26; t[2] &= M26;
-    t[7] += t[6] >> 26; t[6] &= M26;
-    t[4] += t[3] >> 25; t[3] &= M25;
-    t[8] += t[7] >> 25; t[7] &= M25;
-    t[5] += t[4] >> 26; t[4] &= M26;
-    t[9] += t[8] >> 26; t[8] &= M26;
-    t[0] += (t[9] >> 25) * 19u; t[9] &= M25;
-    t[1] += t[0] >> 26; t[0] &= M26;
-#pragma unroll
-    for (int i = 0; i < 10; i++) h.v[i] = (uint32_t)t[i];
-    fe_check_reduced(h);
-}
-
-// Weak reduction of 32-bit limbs (each < 2^31) back to the reduced range.
+// One parallel carry pass: any limbs < 2^32 -> R (every carry < 2^7, 19 * carry9 < 2^12).
 PV_HD void fe_carry(fe& h, const fe& f) {
-    uint32_t t[10];
+    uint32_t c[10], t[10];
 #pragma unroll
-    for (int i = 0; i < 10; i++) t[i] = f.v[i];
-    t[1] += t[0] >> 26; t[0] &= M26;
-    t[5] += t[4] >> 26; t[4] &= M26;
-    t[2] += t[1] >> 25; t[1] &= M25;
-    t[6] += t[5] >> 25; t[5] &= M25;
-    t[3] += t[2] >> 26; t[2] &= M26;
-    t[7] += t[6] >> 26; t[6] &= M26;
-    t[4] += t[3] >> 25; t[3] &= M25;
-    t[8] += t[7] >> 25; t[7] &= M25;
-    t[5] += t[4] >> 26; t[4] &= M26;
-    t[9] += t[8] >> 26; t[8] &= M26;
-    t[0] += (t[9] >> 25) * 19u; t[9] &= M25;
-    t[1] += t[0] >> 26; t[0] &= M26;
+    for (int i = 0; i < 10; i++) {
+        c[i] = f.v[i] >> ((i & 1) ? 25 : 26);
+        t[i] = f.v[i] & ((i & 1) ? M25 : M26);
+    }
+    h.v[0] = t[0] + 19u * c[9];
 #pragma unroll
-    for (int i = 0; i < 10; i++) h.v[i] = t[i];
+    for (int i = 1; i < 10; i++) h.v[i] = t[i] + c[i - 1];
     fe_check_reduced(h);
 }
 
-PV_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
-
-// Keeps the machine scheduler from interleaving independent field multiplications: each one has
-// 55-100 independent v_mad_u64_u32 (ample ILP at 2 waves/SIMD), and interleaving three or four of
-// them multiplies the live accumulators past the 256-VGPR budget (measured: spills to scratch).
-PV_HD void pv_sched_fence() {
-#if defined(__HIP_DEVICE_COMPILE__)
-    __builtin_amdgcn_sched_barrier(0);
+// ------------------------------------------------------------------ multiplication
+#ifdef PV_BOUNDS_CHECK
+#define PV_COL_TRACK(k, a, b) col128[k] += (unsigned __int128)(a) * (b)
+#else
+#define PV_COL_TRACK(k, a, b) do { } while (0)
 #endif
+
+// Folds the carry out of limb 9 (c9 < 2^40) back into limbs 0 and 1: h0 + 19 c9 < 2^45, its carry
+// into limb 1 < 2^19, so the result is R.
+PV_HD void fe_wrap_carry(fe& h, uint64_t c9) {
+    uint64_t r = mad64((uint32_t)c9, 19u, (uint64_t)h.v[0]);
+    r += (uint64_t)((uint32_t)(c9 >> 32) * 19u) << 32;
+    h.v[0] = (uint32_t)r & M26;
+    h.v[1] += (uint32_t)(r >> 26);
 }
 
-// h = f * g
-PV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
-    fe_check_mul_input(f);
-    fe_check_mul_input(g);
-    uint32_t g19[10], f2[10];
+PV_HD void fe_mul19(uint32_t g19[10], const fe& g) {
+    fe_check_g(g);
+#pragma unroll
+    for (int i = 0; i < 10; i++) g19[i] = 19u * g.v[i];
+}
+
+// h = f * g with g19 = 19 * g precomputed (shared operands pay the 10 v_mul_lo_u32 once).
+PV_HD void fe_mul_pre(fe& hout, const fe& f, const fe& g, const uint32_t g19[10]) {
+    fe_check_g(g);
+    fe h;  // hout may alias f or g
+    uint32_t f2[10];
 #pragma unroll
     for (int i = 0; i < 10; i++) {
-        g19[i] = 19u * g.v[i];
-        f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+        f2[i] = (i & 1) ? dbl32(f.v[i]) : f.v[i];
+        PV_ASSERT(f.v[i] < 0x80000000u, "mul f operand");
     }
-    uint64_t t[10];
+#ifdef PV_BOUNDS_CHECK
+    unsigned __int128 col128[10] = {0};
+#endif
+    uint64_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < 10; k++) t[k] = 0;
+    for (int k = 0; k < 10; k++) {
 #pragma unroll
-    for (int i = 0; i < 10; i++) {
-#pragma unroll
-        for (int j = 0; j < 10; j++) {
-            const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-            if (i + j < 10) t[i + j] = mad64(a, g.v[j], t[i + j]);
-            else t[i + j - 10] = mad64(a, g19[j], t[i + j - 10]);
+        for (int i = 0; i < 10; i++) {
+            const int j = k - i;
+            uint32_t a, b;
+            if (j >= 0) {
+                a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+                b = g.v[j];
+            } else {
+                a = ((i & 1) && ((j + 10) & 1)) ? f2[i] : f.v[i];
+                b = g19[j + 10];
+            }
+            PV_COL_TRACK(k, a, b);
+            acc = (k == 0 && i == 0) ? mul64(a, b) : mad64(a, b, acc);
+            if (i == 0 && k > 0) acc = pv_opaque64(acc);
         }
+#ifdef PV_BOUNDS_CHECK
+        if (k > 0) col128[k] += col128[k - 1] >> ((k & 1) ? 26 : 25);
+        PV_ASSERT((col128[k] >> 64) == 0, "mul column overflow");
+#endif
+        const int sh = (k & 1) ? 25 : 26;
+        h.v[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
+        acc >>= sh;
     }
-    fe_carry64(h, t);
+    fe_wrap_carry(h, acc);
+    fe_check_reduced(h);
+    hout = h;
+}
+
+PV_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+    uint32_t g19[10];
+    fe_mul19(g19, g);
+    fe_mul_pre(h, f, g, g19);
     pv_sched_fence();
 }
 
-// h = f^2 (55 products)
-PV_HD void fe_sq(fe& h, const fe& f) {
-    fe_check_mul_input(f);
-    uint32_t f2[10], f19[10];
+// h = f^2: 55 products, column by column (pairs i <= j with i + j = k or k + 10).
+PV_HD void fe_sq(fe& hout, const fe& f) {
+    fe_check_g(f);
+    fe h;  // hout may alias f
+    uint32_t f2[10], f4[10], f19[10];
 #pragma unroll
     for (int i = 0; i < 10; i++) {
-        f2[i] = 2u * f.v[i];
+        f2[i] = dbl32(f.v[i]);
+        f4[i] = dbl32(f2[i]);
         f19[i] = 19u * f.v[i];
     }
-    uint64_t t[10];
+#ifdef PV_BOUNDS_CHECK
+    unsigned __int128 col128[10] = {0};
+#endif
+    uint64_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < 10; k++) t[k] = 0;
+    for (int k = 0; k < 10; k++) {
+        bool first = true;
 #pragma unroll
-    for (int i = 0; i < 10; i++) {
+        for (int i = 0; i < 10; i++) {
 #pragma unroll
-        for (int j = i; j < 10; j++) {
-            // coefficient: (i == j ? 1 : 2) * ((i & j & 1) ? 2 : 1) * (i + j >= 10 ? 19 : 1)
-            const int c = (i == j ? 1 : 2) * (((i & j) & 1) ? 2 : 1);  // 1, 2 or 4
-            uint32_t a = (c == 1) ? f.v[i] : (c == 2 ? f2[i] : 2u * f2[i]);
-            const uint32_t b = (i + j >= 10) ? f19[j] : f.v[j];
-            const int k = (i + j >= 10) ? i + j - 10 : i + j;
-            t[k] = mad64(a, b, t[k]);
+            for (int wrap = 0; wrap < 2; wrap++) {
+                const int j = k + 10 * wrap - i;
+                if (j < i || j > 9) continue;
+                // coefficient (i == j ? 1 : 2) * (i, j both odd ? 2 : 1) * (wrapped ? 19 : 1)
+                const int c = (i == j ? 1 : 2) * (((i & j) & 1) ? 2 : 1);
+                const uint32_t a = (c == 1) ? f.v[i] : (c == 2 ? f2[i] : f4[i]);
+                const uint32_t b = wrap ? f19[j] : f.v[j];
+                PV_COL_TRACK(k, a, b);
+                acc = (k == 0 && first) ? mul64(a, b) : mad64(a, b, acc);
+                if (first && k > 0) acc = pv_opaque64(acc);
+                first = false;
+            }
         }
+#ifdef PV_BOUNDS_CHECK
+        if (k > 0) col128[k] += col128[k - 1] >> ((k & 1) ? 26 : 25);
+        PV_ASSERT((col128[k] >> 64) == 0, "sq column overflow");
+#endif
+        const int sh = (k & 1) ? 25 : 26;
+        h.v[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
+        acc >>= sh;
     }
-    fe_carry64(h, t);
+    fe_wrap_carry(h, acc);
+    fe_check_reduced(h);
+    hout = h;
     pv_sched_fence();
-}
-
-// h = 2 f^2
-PV_HD void fe_sq2(fe& h, const fe& f) {
-    fe t;
-    fe_sq(t, f);
-    fe_add(t, t, t);
-    fe_carry(h, t);
 }
 
 // h = f^(2^n)

@@ -33,36 +33,55 @@ PV_HD void fe_const(fe& h, const uint32_t c[10]) {
     for (int i = 0; i < 10; i++) h.v[i] = c[i];
 }
 
-// r = 2 * p (p: X, Y, Z reduced). Output limbs are valid mul inputs.
+// r = 2 (X : Y : Z), X, Y, Z in R (dbl-2008-hwcd, 4S). Output p1p1, bounds chosen so that only
+// ONE carry pass is needed:
+//   r.X = (X+Y)^2 + 4p - (YY+XX)   uncarried, limbs < 2^28.4: only ever an f operand
+//   r.Y = YY + XX                  < 2^27 + 2^18
+//   r.Z = YY + 2p - XX             < 3 * 2^w + 2^17  (< PV_GMAX)
+//   r.T = 2 ZZ + 4p - r.Z          carried (R)
 PV_HD void ge_p2_dbl(ge_p1p1& r, const fe& X, const fe& Y, const fe& Z) {
-    fe XX, YY, B, S, t;
+    fe XX, YY, ZZ, S, t;
+    fe_add(t, X, Y);
     fe_sq(XX, X);
     fe_sq(YY, Y);
-    fe_sq2(B, Z);
-    fe_add(t, X, Y);
+    fe_add(r.Y, YY, XX);
+    fe_sub(r.Z, YY, XX);
     fe_sq(S, t);
-    fe_add(r.Y, YY, XX);          // YY + XX            (R + R)
-    fe_sub(r.Z, YY, XX);          // YY - XX            (R - R)
-    fe_sub4p(t, S, r.Y);          // S - YY - XX = 2XY
-    fe_carry(r.X, t);
-    fe_sub4p(t, B, r.Z);          // 2Z^2 - YY + XX
+    fe_sub4p(r.X, S, r.Y);
+    fe_sq(ZZ, Z);
+    fe_add(t, ZZ, ZZ);
+    fe_sub4p(t, t, r.Z);
     fe_carry(r.T, t);
 }
 
+// p1p1 -> p2 / p3. g operands (19-multiplied, shared): T and Z for p2, plus Y for p3; X is always
+// the f side, so r.X may be uncarried (ge_p2_dbl) and T/Z/Y only need limbs < PV_GMAX.
 PV_HD void ge_p1p1_to_p2(fe& X, fe& Y, fe& Z, const ge_p1p1& p) {
-    fe_mul(X, p.X, p.T);
-    fe_mul(Y, p.Y, p.Z);
-    fe_mul(Z, p.Z, p.T);
+    uint32_t g19[10];
+    fe_mul19(g19, p.Z);
+    fe_mul_pre(Y, p.Y, p.Z, g19);
+    pv_sched_fence();
+    fe_mul19(g19, p.T);
+    fe_mul_pre(X, p.X, p.T, g19);
+    pv_sched_fence();
+    fe_mul_pre(Z, p.Z, p.T, g19);
+    pv_sched_fence();
 }
 
 PV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
-    fe_mul(r.X, p.X, p.T);
-    fe_mul(r.Y, p.Y, p.Z);
-    fe_mul(r.Z, p.Z, p.T);
+    uint32_t g19[10];
+    fe_mul19(g19, p.T);
+    fe_mul_pre(r.X, p.X, p.T, g19);
+    pv_sched_fence();
+    fe_mul_pre(r.Z, p.Z, p.T, g19);
+    pv_sched_fence();
+    fe_mul19(g19, p.Z);
+    fe_mul_pre(r.Y, p.Y, p.Z, g19);
+    pv_sched_fence();
     fe_mul(r.T, p.X, p.Y);
 }
 
-// r = p + q  (q cached, possibly negated by the caller)
+// r = p + q  (q cached, possibly negated by the caller; p in R). Output limbs < 3 * 2^w + 2^18.
 PV_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
     fe a, b, c, d, t;
     fe_sub(t, p.Y, p.X);
@@ -77,7 +96,8 @@ PV_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
     fe_sub(r.T, d, c);            // F
 }
 
-// r = p + q  (q affine niels, Z = 1)
+// r = p + q  (q affine niels, Z = 1). 2Z is not carried, so F = 2Z + 2p - c has limbs up to
+// 2^28: the result must go through ge_niels_p1p1_to_p2, which keeps F on the f side.
 PV_HD void ge_add_niels(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
     fe a, b, c, d, t;
     fe_sub(t, p.Y, p.X);
@@ -85,12 +105,24 @@ PV_HD void ge_add_niels(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
     fe_add(t, p.Y, p.X);
     fe_mul(b, t, q.yplusx);
     fe_mul(c, p.T, q.xy2d);
-    fe_add(t, p.Z, p.Z);
-    fe_carry(d, t);               // 2 Z, reduced
+    fe_add(d, p.Z, p.Z);          // 2 Z
     fe_sub(r.X, b, a);
     fe_add(r.Y, b, a);
     fe_add(r.Z, d, c);
     fe_sub(r.T, d, c);
+}
+
+// p1p1 -> p2 for a ge_add_niels result: X = E F, Y = H G, Z = G F with E and G as g operands.
+PV_HD void ge_niels_p1p1_to_p2(fe& X, fe& Y, fe& Z, const ge_p1p1& p) {
+    uint32_t g19[10];
+    fe_mul19(g19, p.X);
+    fe_mul_pre(X, p.T, p.X, g19);
+    pv_sched_fence();
+    fe_mul19(g19, p.Z);
+    fe_mul_pre(Y, p.Y, p.Z, g19);
+    pv_sched_fence();
+    fe_mul_pre(Z, p.T, p.Z, g19);
+    pv_sched_fence();
 }
 
 PV_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {

@@ -22,33 +22,56 @@
 #include "../../include/plenum_verify.h"
 
 static constexpr int PV_BLOCK = 256;
+#ifndef PV_MSM_MINBLOCKS
+#define PV_MSM_MINBLOCKS 2  // workgroups per CU the msm kernel's register budget is sized for
+#endif
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per kernel pair (workspace ~1.6 GB)
 
 // ---------------------------------------------------------------------------------------- device
 
+// Per-lane cached table of [j](-A) in HBM, layout [entry][quad][slot] uint4. Indices are 32-bit
+// (chunk <= 2^20 slots, so (9 * 10 + 9) * 2^20 + slot < 2^32) so each access is a uniform 64-bit base
+// plus one per-lane 32-bit offset instead of ten live 64-bit addresses.
 struct DevATab {
     uint4* base;
-    uint64_t nslots;
-    uint64_t slot;
+    uint32_t nslots;
+    uint32_t slot;
+    __device__ __forceinline__ uint4& at(int j, int q) const {
+        return base[(uint32_t)(j * 10 + q) * nslots + slot];
+    }
     __device__ __forceinline__ void store(int j, const uint32_t w[40]) const {
 #pragma unroll
-        for (int q = 0; q < 10; q++)
-            base[(uint64_t)(j * 10 + q) * nslots + slot] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        for (int q = 0; q < 10; q++) at(j, q) = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
     }
-    __device__ __forceinline__ void load(int j, uint32_t w[40]) const {
+    __device__ __forceinline__ void load_half(int j, int h, uint32_t w[20]) const {
 #pragma unroll
-        for (int q = 0; q < 10; q++) {
-            const uint4 v = base[(uint64_t)(j * 10 + q) * nslots + slot];
+        for (int q = 0; q < 5; q++) {
+            const uint4 v = at(j, 5 * h + q);
             w[4 * q] = v.x;
             w[4 * q + 1] = v.y;
             w[4 * q + 2] = v.z;
             w[4 * q + 3] = v.w;
         }
     }
+    __device__ __forceinline__ void load(int j, uint32_t w[40]) const {
+        load_half(j, 0, w);
+        load_half(j, 1, w + 20);
+    }
 };
 
 struct LdsBTab {
     const uint32_t* base;  // LDS
+    __device__ __forceinline__ void load_part(int j, int part, uint32_t w[20]) const {
+        const uint4* e = reinterpret_cast<const uint4*>(base + j * PV_BTAB_STRIDE + 20 * part);
+#pragma unroll
+        for (int i = 0; i < (part ? 3 : 5); i++) {
+            const uint4 v = e[i];
+            if (4 * i < (part ? 10 : 20)) w[4 * i] = v.x;
+            if (4 * i + 1 < (part ? 10 : 20)) w[4 * i + 1] = v.y;
+            if (4 * i + 2 < (part ? 10 : 20)) w[4 * i + 2] = v.z;
+            if (4 * i + 3 < (part ? 10 : 20)) w[4 * i + 3] = v.w;
+        }
+    }
     __device__ __forceinline__ void load(int j, ge_niels& q) const {
         const uint4* e = reinterpret_cast<const uint4*>(base + j * PV_BTAB_STRIDE);
         uint32_t w[32];
@@ -67,6 +90,16 @@ struct LdsBTab {
             q.xy2d.v[i] = w[20 + i];
         }
     }
+};
+
+// Digit words of k (radix 16, rows 0..7) and S (radix 256, rows 8..15), one coalesced load each time
+// the Straus loop enters a new group of 8 windows.
+struct DevDigits {
+    const uint32_t* base;
+    uint32_t stride;
+    uint32_t slot;
+    __device__ __forceinline__ uint32_t ek(int q) const { return base[(uint32_t)q * stride + slot]; }
+    __device__ __forceinline__ uint32_t fs(int q) const { return base[(uint32_t)(8 + q) * stride + slot]; }
 };
 
 // Request bytes at an arbitrary byte offset: aligned dword loads + v_alignbyte_b32 funnel shifts.
@@ -126,7 +159,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __r
         w[20 + q] = negA.Z.v[q];
         w[30 + q] = negA.T.v[q];
     }
-    const DevATab at{wk.atab, wk.stride, i};
+    const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
     at.store(1, w);
     uint32_t ek[8], fs[8];
     sc_recode16(ek, k);
@@ -143,7 +176,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __r
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk) {
     const uint64_t i = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
     if (i >= n) return;
-    const DevATab at{wk.atab, wk.stride, i};
+    const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
     uint32_t w[40];
     at.load(1, w);
     ge_p3 negA;
@@ -158,7 +191,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work 
 }
 
 // Kernel 2: Q = [S]B + [k](-A) by the regular-window Straus loop, encode, compare with R, ballot.
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_msm_kernel(const uint8_t* __restrict__ sm,
+__global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(const uint8_t* __restrict__ sm,
                                                               const uint64_t* __restrict__ off, uint64_t n,
                                                               const uint32_t* __restrict__ btab_g, Work wk,
                                                               uint64_t* __restrict__ verdict) {
@@ -169,16 +202,11 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_msm_kernel(const uint8_t* __re
     const uint64_t i0 = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
     const bool active = i0 < n;
     const uint64_t i = active ? i0 : n - 1;
-    const DevATab at{wk.atab, wk.stride, i};
+    const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
     const LdsBTab bt{sbt};
-    uint32_t ek[8], fs[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-        ek[q] = wk.digits[(uint64_t)q * wk.stride + i];
-        fs[q] = wk.digits[(uint64_t)(8 + q) * wk.stride + i];
-    }
+    const DevDigits dig{wk.digits, (uint32_t)wk.stride, (uint32_t)i};
     uint32_t enc[8];
-    pv_straus(enc, at, bt, ek, fs);
+    pv_straus(enc, at, bt, dig);
     const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[i]);
     const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
     uint32_t R[8];

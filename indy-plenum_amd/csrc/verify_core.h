@@ -102,33 +102,89 @@ PV_HD void pv_build_a_table(ATab& tab, const ge_p3& negA) {
     }
 }
 
-// Signed 4-bit digit at the top of a packed 256-bit nibble string, then shift it out.
-PV_HD int pv_take_top4(uint32_t e[8]) {
-    const int d = ((int32_t)e[7]) >> 28;
+// Signed digit i of the packed recodings: nibble i of ek (radix 16), byte i of fs (radix 256).
+PV_HD int pv_nibble(uint32_t word, int i) { return ((int32_t)(word << (28 - 4 * (i & 7)))) >> 28; }
+PV_HD int pv_byte(uint32_t word, int i) { return ((int32_t)(word << (24 - 8 * (i & 3)))) >> 24; }
+
+// A-table lookups come in two halves so that only 20 words of the entry are live at a time:
+// half 0 = (Y+X, Y-X), half 1 = (2Z, 2dT) of [|e|](-A); negative digits swap Y+X / Y-X and negate
+// 2dT. r = acc + [e](-A) as a p1p1 point (ge_add_cached with the loads interleaved).
+template <class ATab>
+PV_HD void pv_add_a(ge_p1p1& r, const ge_p3& p, const ATab& atab, int e) {
+    const int j = e < 0 ? -e : e;
+    const bool neg = e < 0;
+    fe ypx, ymx, t, a, b, c, d;
+    uint32_t w[20];
+    atab.load_half(j, 0, w);
 #pragma unroll
-    for (int i = 7; i > 0; i--) e[i] = (e[i] << 4) | (e[i - 1] >> 28);
-    e[0] <<= 4;
-    return d;
-}
-PV_HD int pv_take_top8(uint32_t f[8]) {
-    const int d = ((int32_t)f[7]) >> 24;
+    for (int i = 0; i < 10; i++) {
+        ypx.v[i] = neg ? w[10 + i] : w[i];
+        ymx.v[i] = neg ? w[i] : w[10 + i];
+    }
+    fe_sub(t, p.Y, p.X);
+    fe_mul(a, t, ymx);
+    fe_add(t, p.Y, p.X);
+    fe_mul(b, t, ypx);
+    fe z2, t2d;
+    atab.load_half(j, 1, w);
 #pragma unroll
-    for (int i = 7; i > 0; i--) f[i] = (f[i] << 8) | (f[i - 1] >> 24);
-    f[0] <<= 8;
-    return d;
+    for (int i = 0; i < 10; i++) {
+        z2.v[i] = w[i];
+        t2d.v[i] = w[10 + i];
+    }
+    fe_cneg(t2d, t2d, neg);
+    fe_mul(c, p.T, t2d);
+    fe_mul(d, p.Z, z2);
+    fe_sub(r.X, b, a);            // E
+    fe_add(r.Y, b, a);            // H
+    fe_add(r.Z, d, c);            // G
+    fe_sub(r.T, d, c);            // F
 }
 
-// Q = [S]B + [k]A' (A' = -A, tabulated) from the packed signed digits of k (ek, radix 16) and
-// S (fs, radix 256); returns encode(Q) in out[8]. ek/fs are consumed.
-template <class ATab, class BTab>
-PV_HD void pv_straus(uint32_t out[8], ATab& atab, BTab& btab, uint32_t ek[8], uint32_t fs[8]) {
+// r = acc + [f]B (B-table entry in affine niels form, loaded in two parts like pv_add_a).
+template <class BTab>
+PV_HD void pv_add_b(ge_p1p1& r, const ge_p3& p, const BTab& btab, int f) {
+    const int j = f < 0 ? -f : f;
+    const bool neg = f < 0;
+    fe ypx, ymx, xy2d, t, a, b, c, d;
+    uint32_t w[20];
+    btab.load_part(j, 0, w);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        ypx.v[i] = neg ? w[10 + i] : w[i];
+        ymx.v[i] = neg ? w[i] : w[10 + i];
+    }
+    fe_sub(t, p.Y, p.X);
+    fe_mul(a, t, ymx);
+    fe_add(t, p.Y, p.X);
+    fe_mul(b, t, ypx);
+    btab.load_part(j, 1, w);
+#pragma unroll
+    for (int i = 0; i < 10; i++) xy2d.v[i] = w[i];
+    fe_cneg(xy2d, xy2d, neg);
+    fe_mul(c, p.T, xy2d);
+    fe_add(d, p.Z, p.Z);          // 2 Z, not carried (see ge_add_niels)
+    fe_sub(r.X, b, a);
+    fe_add(r.Y, b, a);
+    fe_add(r.Z, d, c);
+    fe_sub(r.T, d, c);
+}
+
+// Q = [S]B + [k]A' (A' = -A, tabulated) from the packed signed digits of k (radix 16) and
+// S (radix 256), read from dig one 32-bit word (8 windows) at a time; returns encode(Q) in out[8].
+template <class ATab, class BTab, class Dig>
+PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const Dig& dig) {
     ge_p3 acc;
     ge_p3_identity(acc);
     ge_p1p1 t;
     fe X, Y, Z;
-    uint32_t w[40];
+    uint32_t ekw = 0, fsw = 0;
     for (int win = 63; win >= 0; win--) {
-        const int e = pv_take_top4(ek);
+        if ((win & 7) == 7) {
+            ekw = dig.ek(win >> 3);
+            fsw = dig.fs(win >> 3);
+        }
+        const int e = pv_nibble(ekw, win);
         if (win != 63) {
             for (int j = 0; j < 3; j++) {
                 ge_p2_dbl(t, X, Y, Z);
@@ -137,31 +193,33 @@ PV_HD void pv_straus(uint32_t out[8], ATab& atab, BTab& btab, uint32_t ek[8], ui
             ge_p2_dbl(t, X, Y, Z);
             ge_p1p1_to_p3(acc, t);
         }
-        ge_cached ca;
-        atab.load(e < 0 ? -e : e, w);
-        ge_cached_load_words(ca, w);
-        ge_cached_cneg(ca, e < 0);
-        ge_add_cached(t, acc, ca);
+        pv_add_a(t, acc, atab, e);
         if ((win & 1) == 0) {
-            const int f = pv_take_top8(fs);
+            const int f = pv_byte(fsw, win >> 1);
             ge_p1p1_to_p3(acc, t);
-            ge_niels nb;
-            btab.load(f < 0 ? -f : f, nb);
-            ge_niels_cneg(nb, f < 0);
-            ge_add_niels(t, acc, nb);
+            pv_add_b(t, acc, btab, f);
+            ge_niels_p1p1_to_p2(X, Y, Z, t);
+        } else {
+            ge_p1p1_to_p2(X, Y, Z, t);
         }
-        ge_p1p1_to_p2(X, Y, Z, t);
     }
     ge_p2_tobytes(out, X, Y, Z);
 }
 
+// Digit words held in registers (host tests and small callers).
+struct pv_dig_regs {
+    uint32_t e[8], f[8];
+    PV_HD uint32_t ek(int q) const { return e[q]; }
+    PV_HD uint32_t fs(int q) const { return f[q]; }
+};
+
 template <class ATab, class BTab>
-PV_HD void pv_double_scalarmult(uint32_t out[8], ATab& atab, BTab& btab, const uint32_t k[8],
+PV_HD void pv_double_scalarmult(uint32_t out[8], const ATab& atab, const BTab& btab, const uint32_t k[8],
                                 const uint32_t S[8]) {
-    uint32_t ek[8], fs[8];
-    sc_recode16(ek, k);
-    sc_recode256(fs, S);
-    pv_straus(out, atab, btab, ek, fs);
+    pv_dig_regs dig;
+    sc_recode16(dig.e, k);
+    sc_recode256(dig.f, S);
+    pv_straus(out, atab, btab, dig);
 }
 
 // Stage 1 of a verification: the checks, A decompression and k. Returns false if any libsodium

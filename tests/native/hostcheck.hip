@@ -48,6 +48,7 @@ struct HostATab {
     uint32_t e[9][40];
     void store(int j, const uint32_t w[40]) { memcpy(e[j], w, 160); }
     void load(int j, uint32_t w[40]) const { memcpy(w, e[j], 160); }
+    void load_half(int j, int h, uint32_t w[20]) const { memcpy(w, e[j] + 20 * h, 80); }
 };
 
 struct HostMsg {

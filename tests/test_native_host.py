@@ -71,6 +71,21 @@ def test_fe_mul_sq_random_and_extreme(hc):
         assert from_limbs(list(h)) % P == from_limbs(f) ** 2 % P
 
 
+def test_fe_mul_wide_f_operand_bounds(hc):
+    """The f side of fe_mul may be an uncarried value (ge_p2_dbl's r.X = S + 4p - r.Y, the niels
+    F = 2Z + 2p - c): at those maxima, against the largest g each call site passes, every
+    product column still fits 64 bits (the bounds build asserts it) and the product is right."""
+    R = [(1 << w) + (1 << 17) - 1 for w in W]                       # reduced output bound
+    G3 = [3 * (1 << w) + (1 << 18) - 1 for w in W]                  # sum / difference of R values
+    dbl_rx = [R[i] + (0xFFFFFB4 if i == 0 else (0x7FFFFFC if i % 2 else 0xFFFFFFC)) for i in range(10)]
+    niels_f = [2 * R[i] + (0x7FFFFDA if i == 0 else (0x3FFFFFE if i % 2 else 0x7FFFFFE)) for i in range(10)]
+    h = A10()
+    for f, g in [(dbl_rx, R), (niels_f, G3), (G3, G3)]:
+        hc.hc_fe_mul(h, A10(*f), A10(*g))
+        assert from_limbs(list(h)) % P == from_limbs(f) * from_limbs(g) % P
+        assert all(v < (1 << w) + (1 << 19) for v, w in zip(h, W))
+
+
 def test_fe_tobytes_canonical_edges(hc):
     s = ctypes.create_string_buffer(32)
     for v in [0, 1, 18, 19, P - 1, P, P + 1, P + 18, 2 ** 255 - 1]:
