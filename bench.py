@@ -117,7 +117,7 @@ def pmc_traffic():
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        return d.get("kernels", {}).get("pv_msm_kernel", {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -191,9 +191,10 @@ def main():
         step()
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    prep_ms, table_ms, msm_ms, launches = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
-    _native.check(L.pv_kernel_times(ctypes.byref(prep_ms), ctypes.byref(table_ms), ctypes.byref(msm_ms),
-                                    ctypes.byref(launches)), "pv_kernel_times")
+    stage = (ctypes.c_double * len(_native.PV_STAGES))()
+    launches = ctypes.c_int()
+    _native.check(L.pv_stage_times(stage, len(_native.PV_STAGES), ctypes.byref(launches)), "pv_stage_times")
+    stage_ms = dict(zip(_native.PV_STAGES, list(stage)))
     L.pv_set_timing(0)
     if world > 1:
         import torch
@@ -213,9 +214,9 @@ def main():
     value = total / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     k = max(1, launches.value)
-    msm_avg_ms = msm_ms.value / k
+    msm_avg_ms = stage_ms["msm"] / k
     achieved = BC.MAC_MSM_KERNEL * n / (msm_avg_ms * 1e-3)
-    pipeline_ms = (prep_ms.value + table_ms.value + msm_ms.value) / k
+    pipeline_ms = sum(stage_ms.values()) / k
     per_gpu_rate = n / (pipeline_ms * 1e-3)
 
     result = {
@@ -231,8 +232,8 @@ def main():
                      "unit": "TMAC/s (v_mad_u64_u32 int32 MACs)", "frac": round(achieved / BC.PEAK_MAC_PER_S, 4),
                      "traffic": pmc_traffic(),
                      "algorithmic_mac_per_verify": round(BC.MAC_MSM_KERNEL), "launch_ms": round(msm_avg_ms, 4)},
-        "pipeline": {"prep_ms": round(prep_ms.value / k, 4), "table_ms": round(table_ms.value / k, 4),
-                     "msm_ms": round(msm_avg_ms, 4), "kernel_verifies_per_s_per_gpu": round(per_gpu_rate, 1),
+        "pipeline": {**{s + "_ms": round(v / k, 4) for s, v in stage_ms.items()},
+                     "kernel_verifies_per_s_per_gpu": round(per_gpu_rate, 1),
                      "whole_verify_valu_frac": round(BC.MAC_PER_VERIFY * per_gpu_rate / BC.PEAK_MAC_PER_S, 4),
                      "hbm_staging_GBps": round(BC.ALGO_BYTES_PER_VERIFY * per_gpu_rate / 1e9, 2)},
         "verdicts_ok": ok_local == n and (ok_all is None or ok_all == n * world),

@@ -76,11 +76,24 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
                            uint64_t* d_verdict_words, void* stream);
 
 /* pv_set_timing(1) (re)starts timing: from then on every launch records HIP events on its own
- * stream around each of its kernels. pv_kernel_times returns the device time (ms) summed over all
- * kernel launches since then: prep (checks, SHA-512, reduction, decompression of A), table (the
- * [j](-A) multiples) and msm (the Straus double-scalar multiplication + encode + compare), and the
- * number of launches of each. pv_set_timing(0) stops recording. */
+ * stream at each stage boundary. pv_stage_times returns the device time (ms) of each stage summed
+ * over all launches since then, in this order (PV_STAGE_*):
+ *   KEYS    per-batch key deduplication and per-key expansion (keyed comb path only)
+ *   PREP    per-request checks, SHA-512, reduction mod L, recoding (and decompression of A on the
+ *           Straus path)
+ *   TABLE   per-request [j](-A) multiples (Straus path) / per-key comb tables (comb path)
+ *   MSM     the double-scalar multiplication [S]B + [k](-A) to projective coordinates
+ *   ENCODE  batched inversion, canonical encoding, compare with R, verdict bits
+ * and the number of launches (chunks). pv_kernel_times is the coarse three-way view
+ * (KEYS+PREP, TABLE, MSM+ENCODE). pv_set_timing(0) stops recording. */
+#define PV_STAGE_KEYS 0
+#define PV_STAGE_PREP 1
+#define PV_STAGE_TABLE 2
+#define PV_STAGE_MSM 3
+#define PV_STAGE_ENCODE 4
+#define PV_NSTAGES 5
 int pv_set_timing(int enable);
+int pv_stage_times(double* ms, int max_stages, int* launches);
 int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* launches);
 
 /* Batched base58 decode (Bitcoin alphabet, PyPI base58 2.x b58decode semantics: trailing ASCII

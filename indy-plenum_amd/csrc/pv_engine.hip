@@ -119,10 +119,12 @@ struct DevMsg {
 //   atab  [9 entries][10 quads][n] uint4   cached [j](-A), j = 0..8
 //   digits[16][n] uint32                    radix-16 digits of k (8 words), radix-256 of S (8 words)
 //   flags [n] uint32                        1 = every libsodium pre-check passed
+//   q     [30][n] uint32                    projective Q = (X, Y, Z) from the msm kernel
 struct Work {
     uint4* atab;
     uint32_t* digits;
     uint32_t* flags;
+    uint32_t* q;
     uint64_t stride;  // chunk capacity (requests)
 };
 
@@ -193,8 +195,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work 
 // Kernel 2: Q = [S]B + [k](-A) by the regular-window Straus loop, encode, compare with R, ballot.
 __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(const uint8_t* __restrict__ sm,
                                                               const uint64_t* __restrict__ off, uint64_t n,
-                                                              const uint32_t* __restrict__ btab_g, Work wk,
-                                                              uint64_t* __restrict__ verdict) {
+                                                              const uint32_t* __restrict__ btab_g, Work wk) {
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
     for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
         reinterpret_cast<uint4*>(sbt)[t] = reinterpret_cast<const uint4*>(btab_g)[t];
@@ -205,16 +206,59 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
     const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
     const LdsBTab bt{sbt};
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, (uint32_t)i};
-    uint32_t enc[8];
-    pv_straus(enc, at, bt, dig);
-    const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[i]);
-    const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
-    uint32_t R[8];
+    fe X, Y, Z;
+    pv_straus_xyz(X, Y, Z, at, bt, dig);
+    if (active) {
 #pragma unroll
-    for (int q = 0; q < 8; q++) R[q] = mw.dw(q);
-    const bool ok = active && wk.flags[i] != 0 && pv_words_equal(enc, R);
-    const uint64_t bits = __ballot(ok);
-    if ((threadIdx.x & 63) == 0 && i0 < n) verdict[i0 >> 6] = bits;
+        for (int q = 0; q < 10; q++) {
+            wk.q[(uint32_t)q * (uint32_t)wk.stride + (uint32_t)i] = X.v[q];
+            wk.q[(uint32_t)(10 + q) * (uint32_t)wk.stride + (uint32_t)i] = Y.v[q];
+            wk.q[(uint32_t)(20 + q) * (uint32_t)wk.stride + (uint32_t)i] = Z.v[q];
+        }
+    }
+}
+
+// Kernel 3: encode Q for PV_ENC_BATCH requests per lane with one shared inversion, compare with R,
+// one __ballot per request group. Wave w covers requests [256 w, 256 w + 256): lane l handles
+// 256 w + l + 64 t, t = 0..3, so every load is coalesced and group t's ballot is verdict word 4 w + t.
+static constexpr int PV_ENC_PER_WAVE = 64 * PV_ENC_BATCH;
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* __restrict__ sm,
+                                                                 const uint64_t* __restrict__ off, uint64_t n,
+                                                                 Work wk, uint64_t* __restrict__ verdict) {
+    const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
+    const uint32_t w = g >> 6, l = g & 63;
+    fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
+    bool use[PV_ENC_BATCH];
+    const uint32_t S = (uint32_t)wk.stride;
+#pragma unroll
+    for (int t = 0; t < PV_ENC_BATCH; t++) {
+        const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
+        const bool in = r < n;
+        const uint32_t rr = in ? r : 0;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            X[t].v[q] = wk.q[q * S + rr];
+            Y[t].v[q] = wk.q[(10 + q) * S + rr];
+            Z[t].v[q] = wk.q[(20 + q) * S + rr];
+        }
+        use[t] = in && wk.flags[rr] != 0;
+    }
+    uint32_t enc[PV_ENC_BATCH][8];
+    pv_encode_batch(enc, X, Y, Z, use);
+#pragma unroll
+    for (int t = 0; t < PV_ENC_BATCH; t++) {
+        const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
+        const uint32_t rr = r < n ? r : 0;
+        const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[rr]);
+        const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+        uint32_t R[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) R[q] = mw.dw(q);
+        const bool ok = use[t] && pv_words_equal(enc[t], R);
+        const uint64_t bits = __ballot(ok);
+        const uint32_t r0 = w * PV_ENC_PER_WAVE + 64 * t;
+        if (l == 0 && r0 < n) verdict[r0 >> 6] = bits;
+    }
 }
 
 // ------------------------------------------------------------------------------------------ host
@@ -226,15 +270,15 @@ struct Ctx {
     int cus = 0;
     hipStream_t stream = nullptr;
     uint32_t* d_btab = nullptr;
-    Work work{nullptr, nullptr, nullptr, 0};
+    Work work{nullptr, nullptr, nullptr, nullptr, 0};
     // host-entry staging
     uint8_t* h_stage = nullptr;  // pinned
     uint64_t h_stage_cap = 0;
     uint8_t* d_stage = nullptr;
     uint64_t d_stage_cap = 0;
     bool timing = false;
-    // event quadruples (prep start, table start, msm start, msm end), one per chunk launched since
-    // pv_set_timing(1); pv_kernel_times sums them
+    // PV_NSTAGES + 1 events per chunk launched since pv_set_timing(1) (stage boundaries, see
+    // pv_stage_times); unused stages record back-to-back events
     std::vector<hipEvent_t> ev;
     int ev_used = 0;
     ncclComm_t comm = nullptr;
@@ -289,30 +333,42 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
     if (n == 0) return PV_OK;
     const uint64_t cap = g_ctx.work.stride;
     const int nchunks = (int)((n + cap - 1) / cap);
+    constexpr int NE = PV_NSTAGES + 1;
     int evb = 0;
     if (g_ctx.timing) {
         evb = g_ctx.ev_used;
-        int rc = ensure_events(evb + 4 * nchunks);
+        int rc = ensure_events(evb + NE * nchunks);
         if (rc) return rc;
-        g_ctx.ev_used = evb + 4 * nchunks;
+        g_ctx.ev_used = evb + NE * nchunks;
     }
     for (int c = 0; c < nchunks; c++) {
         const uint64_t c0 = (uint64_t)c * cap;
         const uint64_t m = std::min<uint64_t>(cap, n - c0);
         const unsigned grid = (unsigned)((m + PV_BLOCK - 1) / PV_BLOCK);
-        hipEvent_t* e = g_ctx.timing ? &g_ctx.ev[evb + 4 * c] : nullptr;
-        if (e) PV_HIP(hipEventRecord(e[0], stream), PV_ERR_LAUNCH);
+        hipEvent_t* e = g_ctx.timing ? &g_ctx.ev[evb + NE * c] : nullptr;
+        auto mark = [&](int k) -> int {
+            if (e) PV_HIP(hipEventRecord(e[k], stream), PV_ERR_LAUNCH);
+            return PV_OK;
+        };
+        int rc = mark(PV_STAGE_KEYS);
+        if (rc) return rc;
+        if ((rc = mark(PV_STAGE_PREP))) return rc;
         hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                            d_pk + 32 * c0, g_ctx.work);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (e) PV_HIP(hipEventRecord(e[1], stream), PV_ERR_LAUNCH);
+        if ((rc = mark(PV_STAGE_TABLE))) return rc;
         hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (e) PV_HIP(hipEventRecord(e[2], stream), PV_ERR_LAUNCH);
+        if ((rc = mark(PV_STAGE_MSM))) return rc;
         hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                           g_ctx.d_btab, g_ctx.work, d_verdict + c0 / 64);
+                           g_ctx.d_btab, g_ctx.work);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (e) PV_HIP(hipEventRecord(e[3], stream), PV_ERR_LAUNCH);
+        if ((rc = mark(PV_STAGE_ENCODE))) return rc;
+        const unsigned egrid = (unsigned)((m + PV_BLOCK * PV_ENC_BATCH - 1) / (PV_BLOCK * PV_ENC_BATCH));
+        hipLaunchKernelGGL(pv_encode_kernel, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+                           g_ctx.work, d_verdict + c0 / 64);
+        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if ((rc = mark(PV_NSTAGES))) return rc;
     }
     return PV_OK;
 }
@@ -355,6 +411,7 @@ int pv_init(int device) {
     PV_HIP(hipMalloc((void**)&g_ctx.work.atab, S * 9 * 160), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * 16 * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 30 * 4), PV_ERR_ALLOC);
     g_ctx.device = device;
     return PV_OK;
 }
@@ -369,6 +426,7 @@ void pv_shutdown(void) {
     if (g_ctx.work.atab) (void)hipFree(g_ctx.work.atab);
     if (g_ctx.work.digits) (void)hipFree(g_ctx.work.digits);
     if (g_ctx.work.flags) (void)hipFree(g_ctx.work.flags);
+    if (g_ctx.work.q) (void)hipFree(g_ctx.work.q);
     for (hipEvent_t e : g_ctx.ev) (void)hipEventDestroy(e);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx = Ctx();
@@ -380,25 +438,32 @@ int pv_set_timing(int enable) {
     return PV_OK;
 }
 
-int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* launches) {
-    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_kernel_times: call pv_init first");
-    double p = 0, t = 0, m = 0;
-    const int nq = g_ctx.ev_used / 4;
+int pv_stage_times(double* ms, int max_stages, int* launches) {
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_stage_times: call pv_init first");
+    constexpr int NE = PV_NSTAGES + 1;
+    double acc[PV_NSTAGES] = {0};
+    const int nq = g_ctx.ev_used / NE;
     for (int c = 0; c < nq; c++) {
-        hipEvent_t* e = &g_ctx.ev[4 * c];
-        float a = 0, b = 0, d = 0;
-        PV_HIP(hipEventSynchronize(e[3]), PV_ERR_LAUNCH);
-        PV_HIP(hipEventElapsedTime(&a, e[0], e[1]), PV_ERR_LAUNCH);
-        PV_HIP(hipEventElapsedTime(&b, e[1], e[2]), PV_ERR_LAUNCH);
-        PV_HIP(hipEventElapsedTime(&d, e[2], e[3]), PV_ERR_LAUNCH);
-        p += a;
-        t += b;
-        m += d;
+        hipEvent_t* e = &g_ctx.ev[NE * c];
+        PV_HIP(hipEventSynchronize(e[PV_NSTAGES]), PV_ERR_LAUNCH);
+        for (int k = 0; k < PV_NSTAGES; k++) {
+            float t = 0;
+            PV_HIP(hipEventElapsedTime(&t, e[k], e[k + 1]), PV_ERR_LAUNCH);
+            acc[k] += t;
+        }
     }
-    if (prep_ms) *prep_ms = p;
-    if (table_ms) *table_ms = t;
-    if (msm_ms) *msm_ms = m;
+    for (int k = 0; k < max_stages && k < PV_NSTAGES; k++) ms[k] = acc[k];
     if (launches) *launches = nq;
+    return PV_OK;
+}
+
+int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* launches) {
+    double t[PV_NSTAGES];
+    const int rc = pv_stage_times(t, PV_NSTAGES, launches);
+    if (rc) return rc;
+    if (prep_ms) *prep_ms = t[PV_STAGE_KEYS] + t[PV_STAGE_PREP];
+    if (table_ms) *table_ms = t[PV_STAGE_TABLE];
+    if (msm_ms) *msm_ms = t[PV_STAGE_MSM] + t[PV_STAGE_ENCODE];
     return PV_OK;
 }
 

@@ -173,11 +173,10 @@ PV_HD void pv_add_b(ge_p1p1& r, const ge_p3& p, const BTab& btab, int f) {
 // Q = [S]B + [k]A' (A' = -A, tabulated) from the packed signed digits of k (radix 16) and
 // S (radix 256), read from dig one 32-bit word (8 windows) at a time; returns encode(Q) in out[8].
 template <class ATab, class BTab, class Dig>
-PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const Dig& dig) {
+PV_HD void pv_straus_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const BTab& btab, const Dig& dig) {
     ge_p3 acc;
     ge_p3_identity(acc);
     ge_p1p1 t;
-    fe X, Y, Z;
     uint32_t ekw = 0, fsw = 0;
     for (int win = 63; win >= 0; win--) {
         if ((win & 7) == 7) {
@@ -203,7 +202,49 @@ PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const 
             ge_p1p1_to_p2(X, Y, Z, t);
         }
     }
+}
+
+template <class ATab, class BTab, class Dig>
+PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const Dig& dig) {
+    fe X, Y, Z;
+    pv_straus_xyz(X, Y, Z, atab, btab, dig);
     ge_p2_tobytes(out, X, Y, Z);
+}
+
+// Encodings of PV_ENC_BATCH projective points with ONE field inversion (Montgomery's trick):
+// c_t = z_0 ... z_t, inv = c_last^-1, then z_t^-1 = inv * c_{t-1} and inv *= z_t going down.
+// A point whose use flag is clear (failed pre-checks, or Z = 0 on garbage input) contributes
+// z = 1 so it cannot poison the shared inverse; its encoding is then meaningless and the caller
+// masks its verdict.
+static constexpr int PV_ENC_BATCH = 4;
+PV_HD void pv_encode_batch(uint32_t out[PV_ENC_BATCH][8], const fe X[PV_ENC_BATCH], const fe Y[PV_ENC_BATCH],
+                           const fe Z[PV_ENC_BATCH], bool use[PV_ENC_BATCH]) {
+    fe z[PV_ENC_BATCH], c[PV_ENC_BATCH];
+#pragma unroll
+    for (int t = 0; t < PV_ENC_BATCH; t++) {
+        use[t] = use[t] && !fe_iszero(Z[t]);
+        fe_1(z[t]);
+        fe_cmov(z[t], Z[t], use[t]);
+        if (t == 0) fe_copy(c[0], z[0]);
+        else fe_mul(c[t], c[t - 1], z[t]);
+    }
+    fe inv;
+    fe_invert(inv, c[PV_ENC_BATCH - 1]);
+#pragma unroll
+    for (int t = PV_ENC_BATCH - 1; t >= 0; t--) {
+        fe zi;
+        if (t > 0) {
+            fe_mul(zi, inv, c[t - 1]);
+            fe_mul(inv, inv, z[t]);
+        } else {
+            fe_copy(zi, inv);
+        }
+        fe x, y;
+        fe_mul(x, X[t], zi);
+        fe_mul(y, Y[t], zi);
+        fe_tobytes32(out[t], y);
+        out[t][7] ^= fe_isnegative(x) << 31;
+    }
 }
 
 // Digit words held in registers (host tests and small callers).

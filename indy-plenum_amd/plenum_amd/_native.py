@@ -17,6 +17,8 @@ PV_OK = 0
 PV_BLOB_SLACK = 256
 PV_ABI_VERSION = 1
 
+PV_STAGES = ("keys", "prep", "table", "msm", "encode")  # PV_STAGE_* order
+
 # exported symbol -> (restype, argtypes); kept in sync with include/plenum_verify.h
 _c_u8p = ctypes.POINTER(ctypes.c_uint8)
 _c_u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -32,6 +34,7 @@ SIGNATURES = {
     "pv_verify_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "pv_set_timing": (ctypes.c_int, [ctypes.c_int]),
+    "pv_stage_times": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "pv_kernel_times": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "pv_b58decode_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,

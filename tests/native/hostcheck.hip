@@ -78,6 +78,21 @@ int hc_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     return ok && pv_words_equal(enc, in.R);
 }
 
+// Batched encoding (one shared inversion) of PV_ENC_BATCH projective points given as 30 limbs
+// each (X, Y, Z); use[t] in/out. Writes 32-byte encodings.
+void hc_encode_batch(uint8_t* out, const uint32_t* xyz, int* use) {
+    fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
+    bool u[PV_ENC_BATCH];
+    for (int t = 0; t < PV_ENC_BATCH; t++) {
+        memcpy(X[t].v, xyz + 30 * t, 40); memcpy(Y[t].v, xyz + 30 * t + 10, 40); memcpy(Z[t].v, xyz + 30 * t + 20, 40);
+        u[t] = use[t] != 0;
+    }
+    uint32_t enc[PV_ENC_BATCH][8];
+    pv_encode_batch(enc, X, Y, Z, u);
+    for (int t = 0; t < PV_ENC_BATCH; t++) { memcpy(out + 32 * t, enc[t], 32); use[t] = u[t]; }
+}
+int hc_enc_batch_size(void) { return PV_ENC_BATCH; }
+
 // k = SHA-512(R||A||M) mod L through pv_prepare (exposes the hashing + reduction)
 void hc_prepare_k(uint8_t* kout, const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     std::vector<uint8_t> buf(smlen + 80, 0);

@@ -171,3 +171,37 @@ def test_pipeline_vs_libsodium(hc, sodium, oracle):
         for _ in range(10):
             sm, pk = g.make(cls)
             assert bool(hc.hc_sign_open(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
+
+
+def test_encode_batch_shared_inversion(hc):
+    """pv_encode_batch (one inversion per PV_ENC_BATCH points) == per-point x/z, y/z encoding; a
+    point with its use flag clear or Z = 0 does not disturb the others."""
+    m = hc.hc_enc_batch_size()
+    rng = random.Random(11)
+    for trial in range(200):
+        pts, use, want = [], [], []
+        for t in range(m):
+            x, y, z = (rng.randrange(P) for _ in range(3))
+            z = z or 1
+            kind = rng.randrange(6)
+            u = 1
+            if kind == 0:
+                z, u = 0, 1          # Z = 0 must be dropped by the zero check
+            elif kind == 1:
+                u = 0                # flagged out by the caller
+            pts += to_limbs(x) + to_limbs(y) + to_limbs(z)
+            use.append(u)
+            if u and z:
+                zi = pow(z, P - 2, P)
+                xa, ya = x * zi % P, y * zi % P
+                want.append((ya | ((xa & 1) << 255)).to_bytes(32, "little"))
+            else:
+                want.append(None)
+        xyz = (ctypes.c_uint32 * (30 * m))(*pts)
+        u_arr = (ctypes.c_int * m)(*use)
+        out = ctypes.create_string_buffer(32 * m)
+        hc.hc_encode_batch(out, xyz, u_arr)
+        for t in range(m):
+            assert bool(u_arr[t]) == (want[t] is not None)
+            if want[t] is not None:
+                assert out.raw[32 * t:32 * t + 32] == want[t], (trial, t)

@@ -29,9 +29,9 @@ for it in range(int(os.environ.get("IT", "3"))):
     _native.check(L.pv_verify_batch_device(d_blob, d_off, n, d_pk, d_v, None), "verify")
     _native.check(L.pv_sync(), "sync")
     dt = time.time() - t
-    pm, tm, mm, nl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
-    L.pv_kernel_times(ctypes.byref(pm), ctypes.byref(tm), ctypes.byref(mm), ctypes.byref(nl)); L.pv_set_timing(1)
+    st = (ctypes.c_double * 5)(); nl = ctypes.c_int()
+    L.pv_stage_times(st, 5, ctypes.byref(nl)); L.pv_set_timing(1)
     v = np.zeros((n + 63) // 64, np.uint64); L.pv_memcpy_d2h(v.ctypes.data, d_v, v.nbytes)
     ok = int(np.unpackbits(v.view(np.uint8), bitorder="little")[:n].sum())
-    print({"n": n, "wall_s": round(dt, 4), "verifies_per_s": round(n / dt), "prep_ms": round(pm.value, 2), "table_ms": round(tm.value, 2),
-           "msm_ms": round(mm.value, 2), "valid": ok}, flush=True)
+    print({"n": n, "wall_s": round(dt, 4), "verifies_per_s": round(n / dt),
+           **{k + "_ms": round(v, 3) for k, v in zip(_native.PV_STAGES, st)}, "valid": ok}, flush=True)
