@@ -43,6 +43,15 @@ MAC_PER_VERIFY = MAC_DECOMPRESS + MAC_TABLE + MAC_LOOP + MAC_ENCODE
 # the encoding runs in pv_encode_kernel
 MAC_MSM_KERNEL = MAC_LOOP
 
+# The keyed comb path (indy-plenum_amd/csrc/comb.h) performs a DIFFERENT algorithm for the same
+# verdict: per request 32 cached-form additions of T_A entries (4 M + 4 M to extended) and 32
+# affine-niels additions of T_B entries (3 M + 4 M), the last one to projective (3 M): no
+# doublings. Its kernel's roofline uses its own algorithmic work, counted the same way:
+MAC_COMB_MSM_KERNEL = MAC_PER_MUL * (32 * 8 + 32 * 7 - 1)
+# per distinct key (amortised over the requests that share it): decompression + 31 x 8 doublings
+# (4 S + 3 M, the last of each 8 to extended: +1 M) + 32 x 129 table entries (8 M + 1 M each)
+MAC_COMB_PER_KEY = _mac(_S_DECOMP, _M_DECOMP) + _mac(31 * 8 * 4, 31 * (8 * 3 + 1)) + MAC_PER_MUL * 32 * 129 * 9
+
 # Peak: v_mad_u64_u32 issues once per 4 cycles per wave64 on a SIMD (measured ~5.2 "cycles at
 # 2.4 GHz" under launch overhead and DVFS in profiles/r01_isa_rates.jsonl, and exactly 2x the
 # full-rate v_add_u32 time there); 256 CU x 4 SIMD x 64 lanes / 4 cycles x 2.4 GHz.

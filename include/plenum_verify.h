@@ -92,6 +92,21 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
 #define PV_STAGE_MSM 3
 #define PV_STAGE_ENCODE 4
 #define PV_NSTAGES 5
+/* Arithmetic path for subsequent launches. Both give bit-identical verdicts:
+ *   PV_PATH_STRAUS  per request: decompress A, 9-entry table of [j](-A), regular-window Straus
+ *                   double-scalar multiplication (252 doublings + 96 additions)
+ *   PV_PATH_COMB    per batch: deduplicate keys; per DISTINCT key: decompress and expand a
+ *                   radix-256 comb table; per request: 64 table additions, no doublings
+ *                   (falls back to Straus when a chunk has more distinct keys than the tables hold)
+ *   PV_PATH_AUTO    (default) comb when keys repeat >= 16x on average in a chunk, else Straus;
+ *                   decided on the device, so pv_verify_batch_device stays asynchronous. */
+#define PV_PATH_AUTO 0
+#define PV_PATH_STRAUS 1
+#define PV_PATH_COMB 2
+int pv_set_path(int mode);
+/* The path the most recent chunk took (PV_PATH_STRAUS or PV_PATH_COMB) and its distinct-key count
+ * (0 when no key kernels ran). Synchronises the device. */
+int pv_last_path(int* path, uint32_t* nkeys);
 int pv_set_timing(int enable);
 int pv_stage_times(double* ms, int max_stages, int* launches);
 int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* launches);

@@ -1,0 +1,215 @@
+// Keyed fixed-base comb verification: the second arithmetic path of the engine.
+//
+// Plenum verifies many requests per verification key (one client DID signs many requests; the
+// BASELINE workload draws 1M requests from 1,024 signers). When a batch repeats keys, each DISTINCT
+// key is decompressed once and expanded into a radix-256 comb table
+//     T_A[key][i][d] = [d * 256^i](-A),   i = 0..31, d = 0..128   (cached form, 160 B per entry)
+// and the fixed base likewise (built once at pv_init, affine niels form)
+//     T_B[i][d]      = [d * 256^i] B.
+// With k and S recoded to 32 signed radix-256 digits each, a verification is then
+//     Q = sum_i ( T_B[i][f_i] + T_A[i][e_i] )  = [S]B - [k]A
+// i.e. 64 point additions and NO doublings (the Straus path needs 252 doublings + 96 additions).
+// The encoding / comparison with R is unchanged (pv_encode_batch), so the verdict is the same
+// function of (R, S, A, M) as libsodium's crypto_sign_open (stp_core/crypto/nacl_wrappers.py:108).
+// Per-key work: one decompression, 248 doublings (the chain of bases [256^i](-A)), 4,128 additions.
+#pragma once
+#include "btable.h"
+#include "verify_core.h"
+
+static constexpr int PV_COMB_POS = 32;        // radix-256 digit positions
+static constexpr int PV_COMB_ENT = 129;       // entries per position (|digit| = 0..128)
+static constexpr int PV_COMB_BLOCKS = 8;      // fill work items per (key, position): 16 entries each
+static constexpr int PV_BCOMB_STRIDE = 32;    // words per fixed-base entry (30 used)
+
+// ---------------------------------------------------------------- per-key expansion
+// bases[i] = [256^i](-A) as extended points, i = 0..31: 31 x (7 doublings to p2 + 1 to p3).
+template <class Bases>
+PV_HD void pv_comb_chain(const Bases& out, const ge_p3& negA) {
+    ge_p3 cur = negA;
+    out.store(0, cur);
+    for (int i = 1; i < PV_COMB_POS; i++) {
+        ge_p1p1 t;
+        fe X = cur.X, Y = cur.Y, Z = cur.Z;
+        for (int j = 0; j < 7; j++) {
+            ge_p2_dbl(t, X, Y, Z);
+            ge_p1p1_to_p2(X, Y, Z, t);
+        }
+        ge_p2_dbl(t, X, Y, Z);
+        ge_p1p1_to_p3(cur, t);
+        out.store(i, cur);
+    }
+}
+
+// Entries d = 16 b + 1 .. 16 b + 16 of one position (block b = 0..7; block 0 also writes the
+// identity at d = 0) from the position's base P: start at [16 b] P by double-and-add, then 16
+// additions of P.
+template <class Table>
+PV_HD void pv_comb_fill_block(const Table& tab, const ge_p3& P, int b) {
+    ge_cached cP;
+    ge_p3_to_cached(cP, P);
+    ge_p3 cur;
+    ge_p1p1 t;
+    if (b == 0) {
+        ge_cached id;
+        ge_cached_identity(id);
+        tab.store(0, id);
+        ge_p3_identity(cur);
+    } else {
+        // [b] P for b = 1..7 (top bit first), then 4 doublings -> [16 b] P
+        cur = P;
+        const int top = b >= 4 ? 2 : (b >= 2 ? 1 : 0);
+        for (int bit = top - 1; bit >= 0; bit--) {
+            ge_p2_dbl(t, cur.X, cur.Y, cur.Z);
+            ge_p1p1_to_p3(cur, t);
+            if ((b >> bit) & 1) {
+                ge_add_cached(t, cur, cP);
+                ge_p1p1_to_p3(cur, t);
+            }
+        }
+        fe X = cur.X, Y = cur.Y, Z = cur.Z;
+        for (int j = 0; j < 3; j++) {
+            ge_p2_dbl(t, X, Y, Z);
+            ge_p1p1_to_p2(X, Y, Z, t);
+        }
+        ge_p2_dbl(t, X, Y, Z);
+        ge_p1p1_to_p3(cur, t);
+    }
+    for (int d = 16 * b + 1; d <= 16 * b + 16; d++) {
+        ge_add_cached(t, cur, cP);
+        ge_p1p1_to_p3(cur, t);
+        ge_cached c;
+        ge_p3_to_cached(c, cur);
+        tab.store(d, c);
+    }
+}
+
+// ---------------------------------------------------------------- per-request accumulation
+// acc + sign(e) T[|e|] for a cached-form table entry (pv_add_a's arithmetic, entry via `load`).
+template <class Entry>
+PV_HD void pv_comb_add_cached(ge_p1p1& r, const ge_p3& p, const Entry& ent, int e) {
+    const int j = e < 0 ? -e : e;
+    const bool neg = e < 0;
+    fe ypx, ymx, t, a, b, c, d;
+    uint32_t w[20];
+    ent.load_half(j, 0, w);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        ypx.v[i] = neg ? w[10 + i] : w[i];
+        ymx.v[i] = neg ? w[i] : w[10 + i];
+    }
+    fe_sub(t, p.Y, p.X);
+    fe_mul(a, t, ymx);
+    fe_add(t, p.Y, p.X);
+    fe_mul(b, t, ypx);
+    fe z2, t2d;
+    ent.load_half(j, 1, w);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        z2.v[i] = w[i];
+        t2d.v[i] = w[10 + i];
+    }
+    fe_cneg(t2d, t2d, neg);
+    fe_mul(c, p.T, t2d);
+    fe_mul(d, p.Z, z2);
+    fe_sub(r.X, b, a);
+    fe_add(r.Y, b, a);
+    fe_add(r.Z, d, c);
+    fe_sub(r.T, d, c);
+}
+
+// Q = [S]B + [k](-A) from the comb tables; a(i) / b(i) give the A- and B-table rows of position i
+// (objects with load_half / load_part), ed / fd the packed radix-256 digits of k and S.
+template <class ARows, class BRows, class Dig>
+PV_HD void pv_comb_xyz(fe& X, fe& Y, fe& Z, const ARows& arows, const BRows& brows, const Dig& dig) {
+    ge_p3 acc;
+    ge_p3_identity(acc);
+    ge_p1p1 t;
+    uint32_t ew = 0, fw = 0;
+    for (int i = PV_COMB_POS - 1; i >= 0; i--) {
+        if ((i & 3) == 3) {
+            ew = dig.ek(i >> 2);
+            fw = dig.fs(i >> 2);
+        }
+        const int e = pv_byte(ew, i);
+        const int f = pv_byte(fw, i);
+        pv_comb_add_cached(t, acc, arows.row(i), e);
+        ge_p1p1_to_p3(acc, t);
+        pv_add_b(t, acc, brows.row(i), f);
+        if (i > 0) {
+            ge_niels_p1p1_to_p3(acc, t);
+        } else {
+            ge_niels_p1p1_to_p2(X, Y, Z, t);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- fixed-base comb (host, init)
+// T_B[i][d] = [d 256^i] B in affine niels form (y+x, y-x, 2dxy), canonical limbs, built on the
+// host with one batched inversion (Montgomery's trick over all 32 x 129 entries).
+inline void pv_build_b_comb(uint32_t* out /* PV_COMB_POS * PV_COMB_ENT * PV_BCOMB_STRIDE */) {
+    ge_p3 negB, P;
+    ge_frombytes_negate(negB, PV_B_ENC);
+    P = negB;
+    fe z;
+    fe_0(z);
+    fe_sub(P.X, z, negB.X);
+    fe_carry(P.X, P.X);
+    fe_sub(P.T, z, negB.T);
+    fe_carry(P.T, P.T);
+    const int N = PV_COMB_POS * PV_COMB_ENT;
+    ge_p3* pts = new ge_p3[N];
+    for (int i = 0; i < PV_COMB_POS; i++) {
+        ge_cached cP;
+        ge_p3_to_cached(cP, P);
+        ge_p3 cur;
+        ge_p3_identity(cur);
+        for (int d = 0; d < PV_COMB_ENT; d++) {
+            pts[i * PV_COMB_ENT + d] = cur;
+            ge_p1p1 t;
+            ge_add_cached(t, cur, cP);
+            ge_p1p1_to_p3(cur, t);
+        }
+        // next base: 256 P = 8 doublings
+        for (int j = 0; j < 8; j++) {
+            ge_p1p1 t;
+            ge_p2_dbl(t, P.X, P.Y, P.Z);
+            ge_p1p1_to_p3(P, t);
+        }
+    }
+    // batched inversion of all Z
+    fe* pre = new fe[N];
+    fe acc;
+    fe_1(acc);
+    for (int k = 0; k < N; k++) {
+        pre[k] = acc;
+        fe_mul(acc, acc, pts[k].Z);
+    }
+    fe inv;
+    fe_invert(inv, acc);
+    fe d2;
+    fe_const(d2, PV_D2);
+    for (int k = N - 1; k >= 0; k--) {
+        fe zi, x, y, t, ypx, ymx, xy2d;
+        fe_mul(zi, inv, pre[k]);
+        fe_mul(inv, inv, pts[k].Z);
+        fe_mul(x, pts[k].X, zi);
+        fe_mul(y, pts[k].Y, zi);
+        fe_add(t, y, x);
+        fe_canonical(ypx, t);
+        fe_sub(t, y, x);
+        fe_canonical(ymx, t);
+        fe_mul(t, x, y);
+        fe_mul(t, t, d2);
+        fe_canonical(xy2d, t);
+        uint32_t* e = out + (uint64_t)k * PV_BCOMB_STRIDE;
+        for (int q = 0; q < 10; q++) {
+            e[q] = ypx.v[q];
+            e[10 + q] = ymx.v[q];
+            e[20 + q] = xy2d.v[q];
+        }
+        e[30] = 0;
+        e[31] = 0;
+    }
+    delete[] pre;
+    delete[] pts;
+}

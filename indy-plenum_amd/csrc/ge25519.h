@@ -125,6 +125,21 @@ PV_HD void ge_niels_p1p1_to_p2(fe& X, fe& Y, fe& Z, const ge_p1p1& p) {
     pv_sched_fence();
 }
 
+// p1p1 -> p3 for a ge_add_niels result (F kept on the f side): X = F E, Y = H G, Z = F G, T = H E.
+PV_HD void ge_niels_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
+    uint32_t g19[10];
+    fe_mul19(g19, p.X);
+    fe_mul_pre(r.X, p.T, p.X, g19);
+    pv_sched_fence();
+    fe_mul_pre(r.T, p.Y, p.X, g19);
+    pv_sched_fence();
+    fe_mul19(g19, p.Z);
+    fe_mul_pre(r.Y, p.Y, p.Z, g19);
+    pv_sched_fence();
+    fe_mul_pre(r.Z, p.T, p.Z, g19);
+    pv_sched_fence();
+}
+
 PV_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
     fe d2, t;
     fe_add(r.YplusX, p.Y, p.X);

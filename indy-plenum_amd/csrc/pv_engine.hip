@@ -14,10 +14,12 @@
 #include <string.h>
 #include <algorithm>
 #include <mutex>
+#include <random>
 #include <string>
 #include <vector>
 
 #include "btable.h"
+#include "comb.h"
 #include "verify_core.h"
 #include "../../include/plenum_verify.h"
 
@@ -25,7 +27,9 @@ static constexpr int PV_BLOCK = 256;
 #ifndef PV_MSM_MINBLOCKS
 #define PV_MSM_MINBLOCKS 2  // workgroups per CU the msm kernel's register budget is sized for
 #endif
-static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per kernel pair (workspace ~1.6 GB)
+static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
+static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
+static constexpr uint32_t PV_COMB_MIN_REUSE = 16; // AUTO: comb path iff distinct keys <= requests / 16
 
 // ---------------------------------------------------------------------------------------- device
 
@@ -128,10 +132,46 @@ struct Work {
     uint64_t stride;  // chunk capacity (requests)
 };
 
+// Which arithmetic path a chunk takes, decided ON THE DEVICE from the number of distinct keys the
+// dedup kernels counted (no host round trip): comb iff nkeys <= limit. nkeys == nullptr means
+// the Straus path was forced and no key kernels ran.
+struct Gate {
+    const uint32_t* nkeys;
+    uint32_t limit;
+    __device__ __forceinline__ bool comb() const { return nkeys && *nkeys <= limit; }
+    __device__ __forceinline__ bool straus() const { return !comb(); }
+};
+
+// Keyed comb workspace (comb.h). The hash table maps a 32-byte key to the index of the first
+// request that carried it; slot_id gives the dense key id of an owned slot.
+//   slot     [H] u32   owner request index, PV_EMPTY = free
+//   slot_id  [H] u32   dense key id of an owned slot
+//   req_key  [stride]  the request's slot, then (after pv_key_assign) its key id
+//   nkeys    [1]       distinct keys counted
+//   key_owner[kcap]    a request carrying key id
+//   key_flag [kcap]    libsodium key checks passed (canonical, not small-order, decompresses)
+//   bases    [kcap][32][10] uint4    [256^i](-A), extended
+//   ctab     [kcap][32][129][10] uint4  T_A, cached form
+struct KeyWork {
+    uint32_t* slot;
+    uint32_t* slot_id;
+    uint32_t* req_key;
+    uint32_t* nkeys;
+    uint32_t* key_owner;
+    uint32_t* key_flag;
+    uint4* bases;
+    uint4* ctab;
+    uint32_t hmask;
+    uint32_t kcap;
+    uint32_t seed;
+};
+static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
+
 // Kernel 1: checks, decompression of A, k = SHA-512(R||A||M) mod L, table of [j](-A), recoding.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __restrict__ sm,
                                                                const uint64_t* __restrict__ off, uint64_t n,
-                                                               const uint8_t* __restrict__ pk, Work wk) {
+                                                               const uint8_t* __restrict__ pk, Work wk, Gate gate) {
+    if (!gate.straus()) return;
     const uint64_t i = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint64_t o0 = off[i], o1 = off[i + 1];
@@ -175,7 +215,8 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __r
 }
 
 // Kernel 1b: expand -A (extended, in slot 1) into the cached table [j](-A), j = 0..8.
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk) {
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk, Gate gate) {
+    if (!gate.straus()) return;
     const uint64_t i = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
     if (i >= n) return;
     const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
@@ -195,7 +236,9 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work 
 // Kernel 2: Q = [S]B + [k](-A) by the regular-window Straus loop, encode, compare with R, ballot.
 __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(const uint8_t* __restrict__ sm,
                                                               const uint64_t* __restrict__ off, uint64_t n,
-                                                              const uint32_t* __restrict__ btab_g, Work wk) {
+                                                              const uint32_t* __restrict__ btab_g, Work wk,
+                                                              Gate gate) {
+    if (!gate.straus()) return;
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
     for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
         reinterpret_cast<uint4*>(sbt)[t] = reinterpret_cast<const uint4*>(btab_g)[t];
@@ -214,6 +257,229 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
             wk.q[(uint32_t)q * (uint32_t)wk.stride + (uint32_t)i] = X.v[q];
             wk.q[(uint32_t)(10 + q) * (uint32_t)wk.stride + (uint32_t)i] = Y.v[q];
             wk.q[(uint32_t)(20 + q) * (uint32_t)wk.stride + (uint32_t)i] = Z.v[q];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ keyed comb path (comb.h)
+
+__device__ __forceinline__ void pv_load_pk(uint32_t A[8], const uint8_t* pk, uint32_t i) {
+    const uint4* p4 = reinterpret_cast<const uint4*>(pk + 32 * (uint64_t)i);
+    const uint4 a0 = p4[0], a1 = p4[1];
+    A[0] = a0.x; A[1] = a0.y; A[2] = a0.z; A[3] = a0.w;
+    A[4] = a1.x; A[5] = a1.y; A[6] = a1.z; A[7] = a1.w;
+}
+
+__device__ __forceinline__ uint32_t pv_key_hash(const uint32_t A[8], uint32_t seed) {
+    uint32_t h = seed;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        h = (h ^ A[q]) * 0x9E3779B1u;
+        h ^= h >> 15;
+    }
+    return h;
+}
+
+// Dedup 1/2: open-addressing insert of every request's key; req_key[i] = the key's slot.
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* __restrict__ pk, uint64_t n,
+                                                                  KeyWork kw) {
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t A[8];
+    pv_load_pk(A, pk, i);
+    uint32_t h = pv_key_hash(A, kw.seed) & kw.hmask;
+    for (uint32_t probe = 0; probe <= kw.hmask; probe++) {  // the table is >= 2x the chunk: never full
+        const uint32_t cur = atomicCAS(&kw.slot[h], PV_EMPTY, i);
+        if (cur == PV_EMPTY) break;
+        uint32_t B[8];
+        pv_load_pk(B, pk, cur);
+        if (pv_words_equal(A, B)) break;
+        h = (h + 1) & kw.hmask;
+    }
+    kw.req_key[i] = h;
+}
+
+// Dedup 2/2: the owner request of each occupied slot takes a dense key id.
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, KeyWork kw) {
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = kw.req_key[i];
+    if (kw.slot[s] != i) return;
+    const uint32_t id = atomicAdd(kw.nkeys, 1u);
+    if (id < kw.kcap) {
+        kw.slot_id[s] = id;
+        kw.key_owner[id] = i;
+    }
+}
+
+struct DevBases {
+    uint4* b;  // [32][10]
+    __device__ __forceinline__ void store(int i, const ge_p3& p) const {
+        uint32_t w[40];
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            w[q] = p.X.v[q];
+            w[10 + q] = p.Y.v[q];
+            w[20 + q] = p.Z.v[q];
+            w[30 + q] = p.T.v[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 10; q++) b[i * 10 + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+    __device__ __forceinline__ void load(int i, ge_p3& p) const {
+        uint32_t w[40];
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            const uint4 v = b[i * 10 + q];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            p.X.v[q] = w[q];
+            p.Y.v[q] = w[10 + q];
+            p.Z.v[q] = w[20 + q];
+            p.T.v[q] = w[30 + q];
+        }
+    }
+};
+
+// One position's row of a key's comb table: entries d = 0..128, 10 uint4 (160 B) each.
+struct DevCombRow {
+    uint4* r;
+    __device__ __forceinline__ void store(int d, const ge_cached& c) const {
+        uint32_t w[40];
+        ge_cached_store_words(w, c);
+#pragma unroll
+        for (int q = 0; q < 10; q++) r[d * 10 + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+    __device__ __forceinline__ void load_half(int d, int h, uint32_t w[20]) const {
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const uint4 v = r[d * 10 + 5 * h + q];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+    }
+};
+struct DevCombRows {
+    uint4* base;  // key's table [32][129][10]
+    __device__ __forceinline__ DevCombRow row(int i) const { return DevCombRow{base + (uint32_t)i * PV_COMB_ENT * 10}; }
+};
+
+// One position's row of the fixed-base comb: entries d = 0..128, PV_BCOMB_STRIDE words each.
+struct DevBRow {
+    const uint4* r;
+    __device__ __forceinline__ void load_part(int d, int part, uint32_t w[20]) const {
+        const uint4* e = r + d * (PV_BCOMB_STRIDE / 4) + 5 * part;
+#pragma unroll
+        for (int q = 0; q < (part ? 3 : 5); q++) {
+            const uint4 v = e[q];
+            const int lim = part ? 10 : 20;
+            if (4 * q < lim) w[4 * q] = v.x;
+            if (4 * q + 1 < lim) w[4 * q + 1] = v.y;
+            if (4 * q + 2 < lim) w[4 * q + 2] = v.z;
+            if (4 * q + 3 < lim) w[4 * q + 3] = v.w;
+        }
+    }
+};
+struct DevBRows {
+    const uint4* base;
+    __device__ __forceinline__ DevBRow row(int i) const {
+        return DevBRow{base + (uint32_t)i * PV_COMB_ENT * (PV_BCOMB_STRIDE / 4)};
+    }
+};
+
+// Per distinct key: libsodium's key checks, -A, and the chain of bases [256^i](-A).
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
+                                                                    Gate gate) {
+    if (!gate.comb()) return;
+    const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (id >= *kw.nkeys) return;
+    uint32_t A[8];
+    pv_load_pk(A, pk, kw.key_owner[id]);
+    ge_p3 negA;
+    const bool ok = pv_key_ok_negate(negA, A);
+    kw.key_flag[id] = ok ? 1u : 0u;
+    pv_comb_chain(DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * 10}, negA);
+}
+
+// Per (key, position, block of 16 entries): the comb table rows. Grid-stride over nkeys * 256 items.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_fill_kernel(KeyWork kw, Gate gate) {
+    if (!gate.comb()) return;
+    const uint32_t items = *kw.nkeys * PV_COMB_POS * PV_COMB_BLOCKS;
+    for (uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x; it < items; it += gridDim.x * PV_BLOCK) {
+        const uint32_t id = it / (PV_COMB_POS * PV_COMB_BLOCKS);
+        const int pos = (it / PV_COMB_BLOCKS) % PV_COMB_POS;
+        const int b = it % PV_COMB_BLOCKS;
+        ge_p3 P;
+        DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * 10}.load(pos, P);
+        pv_comb_fill_block(DevCombRow{kw.ctab + ((uint64_t)id * PV_COMB_POS + pos) * PV_COMB_ENT * 10}, P, b);
+    }
+}
+
+// Per request on the comb path: signature checks, k, key id and validity, radix-256 digits of k, S.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t* __restrict__ sm,
+                                                                    const uint64_t* __restrict__ off, uint64_t n,
+                                                                    const uint8_t* __restrict__ pk, Work wk,
+                                                                    KeyWork kw, Gate gate) {
+    if (!gate.comb()) return;
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o0 = off[i], o1 = off[i + 1];
+    const uint64_t smlen = o1 - o0;
+    const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
+    const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+    pv_sig_words in;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        in.R[q] = mw.dw(q);
+        in.S[q] = mw.dw(8 + q);
+    }
+    pv_load_pk(in.A, pk, i);
+    bool ok = pv_sig_ok(in, smlen);
+    uint32_t k[8];
+    pv_hash_k(k, in, smlen, mw);
+    const uint32_t id = kw.slot_id[kw.req_key[i]];
+    ok &= kw.key_flag[id] != 0;
+    kw.req_key[i] = id;
+    uint32_t ek[8], fs[8];
+    sc_recode256(ek, k);
+    sc_recode256(fs, in.S);
+    const uint32_t S = (uint32_t)wk.stride;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        wk.digits[q * S + i] = ek[q];
+        wk.digits[(8 + q) * S + i] = fs[q];
+    }
+    wk.flags[i] = ok ? 1u : 0u;
+}
+
+// Per request on the comb path: Q = sum of 32 T_A and 32 T_B entries (no doublings).
+__global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_comb_msm_kernel(uint64_t n, Work wk, KeyWork kw,
+                                                                                 const uint4* __restrict__ bcomb,
+                                                                                 Gate gate) {
+    if (!gate.comb()) return;
+    const uint32_t i0 = blockIdx.x * PV_BLOCK + threadIdx.x;
+    const bool active = i0 < n;
+    const uint32_t i = active ? i0 : (uint32_t)n - 1;
+    const uint32_t id = kw.req_key[i];
+    const DevCombRows arows{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10};
+    const DevBRows brows{bcomb};
+    const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
+    fe X, Y, Z;
+    pv_comb_xyz(X, Y, Z, arows, brows, dig);
+    if (active) {
+        const uint32_t S = (uint32_t)wk.stride;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            wk.q[q * S + i] = X.v[q];
+            wk.q[(10 + q) * S + i] = Y.v[q];
+            wk.q[(20 + q) * S + i] = Z.v[q];
         }
     }
 }
@@ -271,6 +537,10 @@ struct Ctx {
     hipStream_t stream = nullptr;
     uint32_t* d_btab = nullptr;
     Work work{nullptr, nullptr, nullptr, nullptr, 0};
+    KeyWork kw{};
+    uint32_t last_limit = 0;  // comb-path key limit of the most recent chunk (0: Straus forced)
+    uint4* d_bcomb = nullptr;  // fixed-base comb T_B
+    int path = PV_PATH_AUTO;
     // host-entry staging
     uint8_t* h_stage = nullptr;  // pinned
     uint64_t h_stage_cap = 0;
@@ -352,17 +622,54 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
         };
         int rc = mark(PV_STAGE_KEYS);
         if (rc) return rc;
+        // Path choice: the comb path pays ~one verification's work per 60 requests for each
+        // distinct key (chain + 4,128-entry table), so AUTO takes it when keys repeat >= 16x on
+        // average; the decision itself is made on the device from the dedup count (Gate).
+        uint32_t limit = 0;
+        if (g_ctx.path == PV_PATH_COMB) limit = g_ctx.kw.kcap;
+        else if (g_ctx.path == PV_PATH_AUTO) limit = (uint32_t)std::min<uint64_t>(g_ctx.kw.kcap, m / PV_COMB_MIN_REUSE);
+        Gate gate{nullptr, 0};
+        g_ctx.last_limit = limit;
+        if (limit > 0) {
+            KeyWork& kw = g_ctx.kw;
+            PV_HIP(hipMemsetAsync(kw.slot, 0xFF, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipMemsetAsync(kw.nkeys, 0, 4, stream), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            gate = Gate{kw.nkeys, limit};
+            hipLaunchKernelGGL(pv_key_chain_kernel, dim3((limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0, stream,
+                               d_pk + 32 * c0, kw, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        }
         if ((rc = mark(PV_STAGE_PREP))) return rc;
         hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                           d_pk + 32 * c0, g_ctx.work);
+                           d_pk + 32 * c0, g_ctx.work, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if (limit > 0) {
+            hipLaunchKernelGGL(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+                               d_pk + 32 * c0, g_ctx.work, g_ctx.kw, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        }
         if ((rc = mark(PV_STAGE_TABLE))) return rc;
-        hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work);
+        hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if (limit > 0) {
+            const uint64_t items = (uint64_t)limit * PV_COMB_POS * PV_COMB_BLOCKS;
+            const unsigned fgrid = (unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096);
+            hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, stream, g_ctx.kw, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        }
         if ((rc = mark(PV_STAGE_MSM))) return rc;
         hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                           g_ctx.d_btab, g_ctx.work);
+                           g_ctx.d_btab, g_ctx.work, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if (limit > 0) {
+            hipLaunchKernelGGL(pv_comb_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.kw,
+                               g_ctx.d_bcomb, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        }
         if ((rc = mark(PV_STAGE_ENCODE))) return rc;
         const unsigned egrid = (unsigned)((m + PV_BLOCK * PV_ENC_BATCH - 1) / (PV_BLOCK * PV_ENC_BATCH));
         hipLaunchKernelGGL(pv_encode_kernel, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
@@ -412,6 +719,25 @@ int pv_init(int device) {
     PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * 16 * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 30 * 4), PV_ERR_ALLOC);
+    {
+        KeyWork& kw = g_ctx.kw;
+        const uint64_t H = 2 * S;
+        kw.hmask = (uint32_t)(H - 1);
+        kw.kcap = PV_KEY_CAP;
+        kw.seed = (uint32_t)std::random_device{}() | 1u;
+        PV_HIP(hipMalloc((void**)&kw.slot, H * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.slot_id, H * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.req_key, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.nkeys, 256), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_owner, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * 160), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
+        std::vector<uint32_t> bc((size_t)PV_COMB_POS * PV_COMB_ENT * PV_BCOMB_STRIDE);
+        pv_build_b_comb(bc.data());
+        PV_HIP(hipMalloc((void**)&g_ctx.d_bcomb, bc.size() * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMemcpy(g_ctx.d_bcomb, bc.data(), bc.size() * 4, hipMemcpyHostToDevice), PV_ERR_ALLOC);
+    }
     g_ctx.device = device;
     return PV_OK;
 }
@@ -427,9 +753,33 @@ void pv_shutdown(void) {
     if (g_ctx.work.digits) (void)hipFree(g_ctx.work.digits);
     if (g_ctx.work.flags) (void)hipFree(g_ctx.work.flags);
     if (g_ctx.work.q) (void)hipFree(g_ctx.work.q);
+    for (void* p : {(void*)g_ctx.kw.slot, (void*)g_ctx.kw.slot_id, (void*)g_ctx.kw.req_key, (void*)g_ctx.kw.nkeys,
+                    (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
+                    (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb})
+        if (p) (void)hipFree(p);
     for (hipEvent_t e : g_ctx.ev) (void)hipEventDestroy(e);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     g_ctx = Ctx();
+}
+
+int pv_last_path(int* path, uint32_t* nkeys) {
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_last_path: call pv_init first");
+    uint32_t u = 0;
+    if (g_ctx.last_limit > 0) {
+        PV_HIP(hipStreamSynchronize(g_ctx.stream), PV_ERR_LAUNCH);
+        PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpy(&u, g_ctx.kw.nkeys, 4, hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
+    }
+    if (nkeys) *nkeys = u;
+    if (path) *path = (g_ctx.last_limit > 0 && u <= g_ctx.last_limit) ? PV_PATH_COMB : PV_PATH_STRAUS;
+    return PV_OK;
+}
+
+int pv_set_path(int mode) {
+    if (mode != PV_PATH_AUTO && mode != PV_PATH_STRAUS && mode != PV_PATH_COMB)
+        return fail(PV_ERR_ARG, "pv_set_path: unknown mode");
+    g_ctx.path = mode;
+    return PV_OK;
 }
 
 int pv_set_timing(int enable) {

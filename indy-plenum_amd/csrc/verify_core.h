@@ -263,18 +263,25 @@ PV_HD void pv_double_scalarmult(uint32_t out[8], const ATab& atab, const BTab& b
     pv_straus(out, atab, btab, dig);
 }
 
-// Stage 1 of a verification: the checks, A decompression and k. Returns false if any libsodium
-// pre-check rejects (the caller still runs the arithmetic on harmless data and masks the verdict).
-template <class MsgWord>
-PV_HD bool pv_prepare(ge_p3& negA, uint32_t k[8], const pv_sig_words& in, uint64_t smlen,
-                      const MsgWord& msgword) {
+// libsodium's checks on the signature half of a request: smlen >= 64, S < L, R not small-order.
+PV_HD bool pv_sig_ok(const pv_sig_words& in, uint64_t smlen) {
     bool ok = smlen >= 64;
     ok &= sc_is_canonical(in.S);
     ok &= !pv_has_small_order(in.R);
-    ok &= pv_ge_is_canonical(in.A);
-    ok &= !pv_has_small_order(in.A);
-    ok &= ge_frombytes_negate(negA, in.A);
+    return ok;
+}
 
+// libsodium's checks on the key, then -A by decompression: canonical, not small-order, on the curve.
+PV_HD bool pv_key_ok_negate(ge_p3& negA, const uint32_t A[8]) {
+    bool ok = pv_ge_is_canonical(A);
+    ok &= !pv_has_small_order(A);
+    ok &= ge_frombytes_negate(negA, A);
+    return ok;
+}
+
+// k = SHA-512(R || A || M) mod L.
+template <class MsgWord>
+PV_HD void pv_hash_k(uint32_t k[8], const pv_sig_words& in, uint64_t smlen, const MsgWord& msgword) {
     // SHA-512 over R || A || M: the input is sm with bytes 32..63 (S) replaced by A, so SHA word
     // q >= 8 is sm word q; T = smlen bytes in total.
     const uint64_t T = smlen;
@@ -311,6 +318,16 @@ PV_HD bool pv_prepare(ge_p3& negA, uint32_t k[8], const pv_sig_words& in, uint64
         h[2 * i + 1] = (uint32_t)(le >> 32);
     }
     sc_reduce64(k, h);
+}
+
+// Stage 1 of a verification: the checks, A decompression and k. Returns false if any libsodium
+// pre-check rejects (the caller still runs the arithmetic on harmless data and masks the verdict).
+template <class MsgWord>
+PV_HD bool pv_prepare(ge_p3& negA, uint32_t k[8], const pv_sig_words& in, uint64_t smlen,
+                      const MsgWord& msgword) {
+    bool ok = pv_sig_ok(in, smlen);
+    ok &= pv_key_ok_negate(negA, in.A);
+    pv_hash_k(k, in, smlen, msgword);
     return ok;
 }
 

@@ -18,6 +18,7 @@ PV_BLOB_SLACK = 256
 PV_ABI_VERSION = 1
 
 PV_STAGES = ("keys", "prep", "table", "msm", "encode")  # PV_STAGE_* order
+PV_PATH_AUTO, PV_PATH_STRAUS, PV_PATH_COMB = 0, 1, 2
 
 # exported symbol -> (restype, argtypes); kept in sync with include/plenum_verify.h
 _c_u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -34,6 +35,8 @@ SIGNATURES = {
     "pv_verify_batch_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "pv_set_timing": (ctypes.c_int, [ctypes.c_int]),
+    "pv_set_path": (ctypes.c_int, [ctypes.c_int]),
+    "pv_last_path": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]),
     "pv_stage_times": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "pv_kernel_times": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
@@ -134,3 +137,16 @@ def verify_sm_batch(blob, offsets, pks):
     bits = np.zeros((n + 7) // 8, dtype=np.uint8)
     check(L.pv_verify_batch(_ptr(blob), _ptr(offsets), n, _ptr(pks), _ptr(bits)), "pv_verify_batch")
     return np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+
+
+def set_path(mode):
+    """Select the arithmetic path (PV_PATH_AUTO / PV_PATH_STRAUS / PV_PATH_COMB); verdicts are
+    identical on every path."""
+    check(lib().pv_set_path(int(mode)), "pv_set_path")
+
+
+def last_path():
+    """(path, distinct keys) of the most recent chunk: path is PV_PATH_STRAUS or PV_PATH_COMB."""
+    p, u = ctypes.c_int(), ctypes.c_uint32()
+    check(lib().pv_last_path(ctypes.byref(p), ctypes.byref(u)), "pv_last_path")
+    return p.value, u.value

@@ -4,6 +4,7 @@
 #define PV_BOUNDS_CHECK 1
 #include "verify_core.h"
 #include "btable.h"
+#include "comb.h"
 #include <string.h>
 #include <vector>
 
@@ -92,6 +93,70 @@ void hc_encode_batch(uint8_t* out, const uint32_t* xyz, int* use) {
     for (int t = 0; t < PV_ENC_BATCH; t++) { memcpy(out + 32 * t, enc[t], 32); use[t] = u[t]; }
 }
 int hc_enc_batch_size(void) { return PV_ENC_BATCH; }
+
+// ---- keyed comb path on the host (comb.h): same code the comb kernels run
+struct HostBases {
+    ge_p3* b;
+    void store(int i, const ge_p3& p) const { b[i] = p; }
+};
+struct HostCombRow {
+    uint32_t* r;  // [129][40]
+    void store(int d, const ge_cached& c) const { ge_cached_store_words(r + 40 * d, c); }
+    void load_half(int d, int h, uint32_t w[20]) const { memcpy(w, r + 40 * d + 20 * h, 80); }
+};
+struct HostCombRows {
+    uint32_t* base;
+    HostCombRow row(int i) const { return HostCombRow{base + (size_t)i * PV_COMB_ENT * 40}; }
+};
+struct HostBRow {
+    const uint32_t* r;
+    void load_part(int d, int part, uint32_t w[20]) const {
+        memcpy(w, r + d * PV_BCOMB_STRIDE + 20 * part, part ? 40 : 80);
+    }
+};
+struct HostBRows {
+    const uint32_t* base;
+    HostBRow row(int i) const { return HostBRow{base + (size_t)i * PV_COMB_ENT * PV_BCOMB_STRIDE}; }
+};
+
+// crypto_sign_open through the comb path: key expansion (chain + all fill blocks), radix-256
+// digits, 64 additions, batched encoding.
+int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    static std::vector<uint32_t> bcomb;
+    if (bcomb.empty()) {
+        bcomb.resize((size_t)PV_COMB_POS * PV_COMB_ENT * PV_BCOMB_STRIDE);
+        pv_build_b_comb(bcomb.data());
+    }
+    std::vector<uint8_t> buf(smlen + 80, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    HostMsg mw{buf.data()};
+    bool ok = pv_sig_ok(in, smlen);
+    ge_p3 negA;
+    ok &= pv_key_ok_negate(negA, in.A);
+    uint32_t k[8];
+    pv_hash_k(k, in, smlen, mw);
+    std::vector<ge_p3> bases(PV_COMB_POS);
+    pv_comb_chain(HostBases{bases.data()}, negA);
+    std::vector<uint32_t> ctab((size_t)PV_COMB_POS * PV_COMB_ENT * 40);
+    for (int pos = 0; pos < PV_COMB_POS; pos++)
+        for (int b = 0; b < PV_COMB_BLOCKS; b++)
+            pv_comb_fill_block(HostCombRow{ctab.data() + (size_t)pos * PV_COMB_ENT * 40}, bases[pos], b);
+    pv_dig_regs dig;
+    sc_recode256(dig.e, k);
+    sc_recode256(dig.f, in.S);
+    fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
+    bool use[PV_ENC_BATCH];
+    pv_comb_xyz(X[0], Y[0], Z[0], HostCombRows{ctab.data()}, HostBRows{bcomb.data()}, dig);
+    use[0] = ok;
+    for (int t = 1; t < PV_ENC_BATCH; t++) { X[t] = X[0]; Y[t] = Y[0]; Z[t] = Z[0]; use[t] = false; }
+    uint32_t enc[PV_ENC_BATCH][8];
+    pv_encode_batch(enc, X, Y, Z, use);
+    return use[0] && pv_words_equal(enc[0], in.R);
+}
 
 // k = SHA-512(R||A||M) mod L through pv_prepare (exposes the hashing + reduction)
 void hc_prepare_k(uint8_t* kout, const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {

@@ -39,9 +39,14 @@ def test_config3_1M_adversarial_bit_exact(native, nym1m, oracle):
     from oracle.oracle import cpu_verdicts
     blob, off, pks = nym1m
     blob2, pks2, idx, labels = inject(blob, off, pks, 0.02, seed=3, oracle=oracle)
-    got = native.verify_sm_batch(blob2, off, pks2)
     want = cpu_verdicts(blob2, off, pks2)
-    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    # both arithmetic paths: the per-request Straus path and the keyed comb path (~10k distinct
+    # keys here: the 1,024 signers plus every mutated key)
+    for path in (native.PV_PATH_STRAUS, native.PV_PATH_COMB):
+        native.set_path(path)
+        got = native.verify_sm_batch(blob2, off, pks2)
+        native.set_path(native.PV_PATH_AUTO)
+        assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
     # the untouched 98 % are valid and the mutated records are (almost all) rejected
     mask = np.ones(len(got), bool)
     mask[idx] = False

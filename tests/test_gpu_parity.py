@@ -9,11 +9,14 @@ from vectors import VectorGen, pack
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def native():
+@pytest.fixture(scope="module", params=["straus", "comb"])
+def native(request):
+    """The engine with each arithmetic path forced in turn (verdicts must not depend on it)."""
     from plenum_amd import _native
     _native.ensure_device()
-    return _native
+    _native.set_path(_native.PV_PATH_STRAUS if request.param == "straus" else _native.PV_PATH_COMB)
+    yield _native
+    _native.set_path(_native.PV_PATH_AUTO)
 
 
 def reference_verdicts(sodium, cases):
@@ -62,3 +65,29 @@ def test_empty_and_single(native, sodium, oracle):
         cases = g.batch(n, adversarial_frac=0.3)
         blob, off, pks = pack(cases)
         assert np.array_equal(native.verify_sm_batch(blob, off, pks), reference_verdicts(sodium, cases))
+
+
+def test_repeated_keys_with_adversarial(native, sodium, oracle):
+    """Few distinct keys shared by many requests (the comb path's case), including shared keys that
+    fail libsodium's key checks, honest signatures under mixed-order keys, and per-request
+    signature corruption, at every record alignment."""
+    g = VectorGen(sodium, oracle, seed=15)
+    base = [g.make("valid") for _ in range(40)]
+    bad_keys = [g.make(c)[1] for c in ("A_blacklist", "A_noncanonical", "A_offcurve", "mixed_order_A")]
+    cases = []
+    rng = np.random.default_rng(15)
+    for i in range(4000):
+        sm, pk = base[int(rng.integers(0, len(base)))]
+        r = rng.random()
+        if r < 0.04:
+            pk = bad_keys[int(rng.integers(0, len(bad_keys)))]
+        elif r < 0.08:
+            sm = bytearray(sm)
+            sm[int(rng.integers(0, len(sm)))] ^= 1 << int(rng.integers(0, 8))
+            sm = bytes(sm)
+        cases.append((sm, pk))
+    blob, off, pks = pack(cases)
+    got = native.verify_sm_batch(blob, off, pks)
+    want = reference_verdicts(sodium, cases)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert 0.85 * len(cases) < want.sum() < len(cases)
