@@ -444,9 +444,9 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
     bool ok = pv_sig_ok(in, smlen);
     uint32_t k[8];
     pv_hash_k(k, in, smlen, mw);
-    const uint32_t id = kw.slot_id[kw.req_key[i]];
-    ok &= kw.key_flag[id] != 0;
-    kw.req_key[i] = id;
+    // the key's own checks (key_flag) are written by pv_key_chain_kernel on the key stream, which
+    // runs concurrently with this kernel: pv_comb_msm_kernel folds them into flags[i]
+    kw.req_key[i] = kw.slot_id[kw.req_key[i]];
     uint32_t ek[8], fs[8];
     sc_recode256(ek, k);
     sc_recode256(fs, in.S);
@@ -475,6 +475,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_comb_msm_kernel
     pv_comb_xyz(X, Y, Z, arows, brows, dig);
     if (active) {
         const uint32_t S = (uint32_t)wk.stride;
+        if (kw.key_flag[id] == 0) wk.flags[i] = 0;
 #pragma unroll
         for (int q = 0; q < 10; q++) {
             wk.q[q * S + i] = X.v[q];
@@ -535,6 +536,9 @@ struct Ctx {
     int device = -1;
     int cus = 0;
     hipStream_t stream = nullptr;
+    hipStream_t kstream = nullptr;           // per-key pipeline (chain + table fill), overlapped
+    hipEvent_t ev_keys_ready = nullptr;      // dedup done (main -> kstream)
+    hipEvent_t ev_tables_ready = nullptr;    // comb tables done (kstream -> main)
     uint32_t* d_btab = nullptr;
     Work work{nullptr, nullptr, nullptr, nullptr, 0};
     KeyWork kw{};
@@ -639,9 +643,18 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
             hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             gate = Gate{kw.nkeys, limit};
-            hipLaunchKernelGGL(pv_key_chain_kernel, dim3((limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0, stream,
-                               d_pk + 32 * c0, kw, gate);
+            // the per-key chain (few, long-latency lanes) and the table fill run on kstream,
+            // overlapped with the per-request prep on the main stream
+            PV_HIP(hipEventRecord(g_ctx.ev_keys_ready, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipStreamWaitEvent(g_ctx.kstream, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_key_chain_kernel, dim3((limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
+                               g_ctx.kstream, d_pk + 32 * c0, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            const uint64_t items = (uint64_t)limit * PV_COMB_POS * PV_COMB_BLOCKS;
+            const unsigned fgrid = (unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096);
+            hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, g_ctx.kstream, g_ctx.kw, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.kstream), PV_ERR_LAUNCH);
         }
         if ((rc = mark(PV_STAGE_PREP))) return rc;
         hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
@@ -655,12 +668,7 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
         if ((rc = mark(PV_STAGE_TABLE))) return rc;
         hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (limit > 0) {
-            const uint64_t items = (uint64_t)limit * PV_COMB_POS * PV_COMB_BLOCKS;
-            const unsigned fgrid = (unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096);
-            hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, stream, g_ctx.kw, gate);
-            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        }
+        if (limit > 0) PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
         if ((rc = mark(PV_STAGE_MSM))) return rc;
         hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                            g_ctx.d_btab, g_ctx.work, gate);
@@ -709,6 +717,9 @@ int pv_init(int device) {
         return fail(PV_ERR_NO_DEVICE, std::string("pv_init: built for gfx950, device is ") + prop.gcnArchName);
     g_ctx.cus = prop.multiProcessorCount;
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+    PV_HIP(hipStreamCreateWithFlags(&g_ctx.kstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_keys_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     std::vector<uint32_t> bt(PV_BTAB_ENTRIES * PV_BTAB_STRIDE);
     pv_build_b_table(bt.data());
     PV_HIP(hipMalloc((void**)&g_ctx.d_btab, bt.size() * 4), PV_ERR_ALLOC);
@@ -759,6 +770,9 @@ void pv_shutdown(void) {
         if (p) (void)hipFree(p);
     for (hipEvent_t e : g_ctx.ev) (void)hipEventDestroy(e);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
+    if (g_ctx.kstream) (void)hipStreamDestroy(g_ctx.kstream);
+    if (g_ctx.ev_keys_ready) (void)hipEventDestroy(g_ctx.ev_keys_ready);
+    if (g_ctx.ev_tables_ready) (void)hipEventDestroy(g_ctx.ev_tables_ready);
     g_ctx = Ctx();
 }
 
