@@ -44,10 +44,10 @@ MAC_PER_VERIFY = MAC_DECOMPRESS + MAC_TABLE + MAC_LOOP + MAC_ENCODE
 MAC_MSM_KERNEL = MAC_LOOP
 
 # The keyed comb path (indy-plenum_amd/csrc/comb.h) performs a DIFFERENT algorithm for the same
-# verdict: per request 32 cached-form additions of T_A entries (4 M + 4 M to extended) and 32
-# affine-niels additions of T_B entries (3 M + 4 M), the last one to projective (3 M): no
-# doublings. Its kernel's roofline uses its own algorithmic work, counted the same way:
-MAC_COMB_MSM_KERNEL = MAC_PER_MUL * (32 * 8 + 32 * 7 - 1)
+# verdict: per request 32 cached-form additions of radix-256 T_A entries (4 M + 4 M to extended) and
+# 16 affine-niels additions of radix-65536 T_B entries (3 M + 4 M), the last one to projective
+# (3 M): no doublings. Its kernel's roofline uses its own algorithmic work, counted the same way:
+MAC_COMB_MSM_KERNEL = MAC_PER_MUL * (32 * 8 + 16 * 7 - 1)
 # per distinct key (amortised over the requests that share it): decompression + 31 x 8 doublings
 # (4 S + 3 M, the last of each 8 to extended: +1 M) + 32 x 129 table entries (8 M + 1 M each)
 MAC_COMB_PER_KEY = _mac(_S_DECOMP, _M_DECOMP) + _mac(31 * 8 * 4, 31 * (8 * 3 + 1)) + MAC_PER_MUL * 32 * 129 * 9

@@ -4,11 +4,13 @@
 // BASELINE workload draws 1M requests from 1,024 signers). When a batch repeats keys, each DISTINCT
 // key is decompressed once and expanded into a radix-256 comb table
 //     T_A[key][i][d] = [d * 256^i](-A),   i = 0..31, d = 0..128   (cached form, 160 B per entry)
-// and the fixed base likewise (built once at pv_init, affine niels form)
-//     T_B[i][d]      = [d * 256^i] B.
-// With k and S recoded to 32 signed radix-256 digits each, a verification is then
-//     Q = sum_i ( T_B[i][f_i] + T_A[i][e_i] )  = [S]B - [k]A
-// i.e. 64 point additions and NO doublings (the Straus path needs 252 doublings + 96 additions).
+// and the fixed base with a wider radix, since its table is built once (at pv_init, affine niels
+// form, 67 MB, Infinity-Cache resident)
+//     T_B[j][d]      = [d * 65536^j] B,   j = 0..15, d = 0..32768.
+// With k recoded to 32 signed radix-256 digits and S to 16 signed radix-65536 digits, a
+// verification is then
+//     Q = sum_i T_A[i][e_i] + sum_j T_B[j][f_j]  = [S]B - [k]A
+// i.e. 48 point additions and NO doublings (the Straus path needs 252 doublings + 96 additions).
 // The encoding / comparison with R is unchanged (pv_encode_batch), so the verdict is the same
 // function of (R, S, A, M) as libsodium's crypto_sign_open (stp_core/crypto/nacl_wrappers.py:108).
 // Per-key work: one decompression, 248 doublings (the chain of bases [256^i](-A)), 4,128 additions.
@@ -20,6 +22,8 @@ static constexpr int PV_COMB_POS = 32;        // radix-256 digit positions
 static constexpr int PV_COMB_ENT = 129;       // entries per position (|digit| = 0..128)
 static constexpr int PV_COMB_BLOCKS = 8;      // fill work items per (key, position): 16 entries each
 static constexpr int PV_BCOMB_STRIDE = 32;    // words per fixed-base entry (30 used)
+static constexpr int PV_BCOMB_POS = 16;       // radix-65536 digit positions of S
+static constexpr int PV_BCOMB_ENT = 32769;    // entries per position (|digit| = 0..32768)
 
 // ---------------------------------------------------------------- per-key expansion
 // bases[i] = [256^i](-A) as extended points, i = 0..31: 31 x (7 doublings to p2 + 1 to p3).
@@ -117,8 +121,9 @@ PV_HD void pv_comb_add_cached(ge_p1p1& r, const ge_p3& p, const Entry& ent, int 
     fe_sub(r.T, d, c);
 }
 
-// Q = [S]B + [k](-A) from the comb tables; a(i) / b(i) give the A- and B-table rows of position i
-// (objects with load_half / load_part), ed / fd the packed radix-256 digits of k and S.
+// Q = [S]B + [k](-A) from the comb tables: arows.row(i) / brows.row(j) give the A row of radix-256
+// position i and the B row of radix-65536 position j (objects with load_half / load_part); dig holds
+// the packed digits (ek: 4 signed bytes of k per word, fs: 2 signed halfwords of S per word).
 template <class ARows, class BRows, class Dig>
 PV_HD void pv_comb_xyz(fe& X, fe& Y, fe& Z, const ARows& arows, const BRows& brows, const Dig& dig) {
     ge_p3 acc;
@@ -131,69 +136,52 @@ PV_HD void pv_comb_xyz(fe& X, fe& Y, fe& Z, const ARows& arows, const BRows& bro
             fw = dig.fs(i >> 2);
         }
         const int e = pv_byte(ew, i);
-        const int f = pv_byte(fw, i);
         pv_comb_add_cached(t, acc, arows.row(i), e);
         ge_p1p1_to_p3(acc, t);
-        pv_add_b(t, acc, brows.row(i), f);
-        if (i > 0) {
-            ge_niels_p1p1_to_p3(acc, t);
-        } else {
-            ge_niels_p1p1_to_p2(X, Y, Z, t);
+        if ((i & 1) == 0) {
+            const int f = pv_half(fw, i >> 1);
+            pv_add_b(t, acc, brows.row(i >> 1), f);
+            if (i > 0) {
+                ge_niels_p1p1_to_p3(acc, t);
+            } else {
+                ge_niels_p1p1_to_p2(X, Y, Z, t);
+            }
         }
     }
 }
 
 // ---------------------------------------------------------------- fixed-base comb (host, init)
-// T_B[i][d] = [d 256^i] B in affine niels form (y+x, y-x, 2dxy), canonical limbs, built on the
-// host with one batched inversion (Montgomery's trick over all 32 x 129 entries).
-inline void pv_build_b_comb(uint32_t* out /* PV_COMB_POS * PV_COMB_ENT * PV_BCOMB_STRIDE */) {
-    ge_p3 negB, P;
-    ge_frombytes_negate(negB, PV_B_ENC);
-    P = negB;
-    fe z;
-    fe_0(z);
-    fe_sub(P.X, z, negB.X);
-    fe_carry(P.X, P.X);
-    fe_sub(P.T, z, negB.T);
-    fe_carry(P.T, P.T);
-    const int N = PV_COMB_POS * PV_COMB_ENT;
+// T_B[j][d] = [d 65536^j] B in affine niels form (y+x, y-x, 2dxy), canonical limbs, PV_BCOMB_STRIDE
+// words per entry. Built on the host: one thread per position (16), each with one batched
+// inversion (Montgomery's trick) over its 32,769 entries.
+inline void pv_bcomb_build_position(uint32_t* out, const ge_p3& P) {
+    const int N = PV_BCOMB_ENT;
     ge_p3* pts = new ge_p3[N];
-    for (int i = 0; i < PV_COMB_POS; i++) {
-        ge_cached cP;
-        ge_p3_to_cached(cP, P);
-        ge_p3 cur;
-        ge_p3_identity(cur);
-        for (int d = 0; d < PV_COMB_ENT; d++) {
-            pts[i * PV_COMB_ENT + d] = cur;
-            ge_p1p1 t;
-            ge_add_cached(t, cur, cP);
-            ge_p1p1_to_p3(cur, t);
-        }
-        // next base: 256 P = 8 doublings
-        for (int j = 0; j < 8; j++) {
-            ge_p1p1 t;
-            ge_p2_dbl(t, P.X, P.Y, P.Z);
-            ge_p1p1_to_p3(P, t);
-        }
-    }
-    // batched inversion of all Z
     fe* pre = new fe[N];
+    ge_cached cP;
+    ge_p3_to_cached(cP, P);
+    ge_p3 cur;
+    ge_p3_identity(cur);
     fe acc;
     fe_1(acc);
-    for (int k = 0; k < N; k++) {
-        pre[k] = acc;
-        fe_mul(acc, acc, pts[k].Z);
+    for (int d = 0; d < N; d++) {
+        pts[d] = cur;
+        pre[d] = acc;
+        fe_mul(acc, acc, cur.Z);
+        ge_p1p1 t;
+        ge_add_cached(t, cur, cP);
+        ge_p1p1_to_p3(cur, t);
     }
     fe inv;
     fe_invert(inv, acc);
     fe d2;
     fe_const(d2, PV_D2);
-    for (int k = N - 1; k >= 0; k--) {
+    for (int d = N - 1; d >= 0; d--) {
         fe zi, x, y, t, ypx, ymx, xy2d;
-        fe_mul(zi, inv, pre[k]);
-        fe_mul(inv, inv, pts[k].Z);
-        fe_mul(x, pts[k].X, zi);
-        fe_mul(y, pts[k].Y, zi);
+        fe_mul(zi, inv, pre[d]);
+        fe_mul(inv, inv, pts[d].Z);
+        fe_mul(x, pts[d].X, zi);
+        fe_mul(y, pts[d].Y, zi);
         fe_add(t, y, x);
         fe_canonical(ypx, t);
         fe_sub(t, y, x);
@@ -201,7 +189,7 @@ inline void pv_build_b_comb(uint32_t* out /* PV_COMB_POS * PV_COMB_ENT * PV_BCOM
         fe_mul(t, x, y);
         fe_mul(t, t, d2);
         fe_canonical(xy2d, t);
-        uint32_t* e = out + (uint64_t)k * PV_BCOMB_STRIDE;
+        uint32_t* e = out + (uint64_t)d * PV_BCOMB_STRIDE;
         for (int q = 0; q < 10; q++) {
             e[q] = ypx.v[q];
             e[10 + q] = ymx.v[q];
@@ -212,4 +200,25 @@ inline void pv_build_b_comb(uint32_t* out /* PV_COMB_POS * PV_COMB_ENT * PV_BCOM
     }
     delete[] pre;
     delete[] pts;
+}
+
+// the 16 position bases [65536^j] B, extended
+inline void pv_bcomb_bases(ge_p3 base[PV_BCOMB_POS]) {
+    ge_p3 negB, P;
+    ge_frombytes_negate(negB, PV_B_ENC);
+    P = negB;
+    fe z;
+    fe_0(z);
+    fe_sub(P.X, z, negB.X);
+    fe_carry(P.X, P.X);
+    fe_sub(P.T, z, negB.T);
+    fe_carry(P.T, P.T);
+    for (int j = 0; j < PV_BCOMB_POS; j++) {
+        base[j] = P;
+        for (int r = 0; r < 16; r++) {
+            ge_p1p1 t;
+            ge_p2_dbl(t, P.X, P.Y, P.Z);
+            ge_p1p1_to_p3(P, t);
+        }
+    }
 }

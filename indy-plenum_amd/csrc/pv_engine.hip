@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <mutex>
 #include <random>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -371,7 +372,7 @@ struct DevCombRows {
     __device__ __forceinline__ DevCombRow row(int i) const { return DevCombRow{base + (uint32_t)i * PV_COMB_ENT * 10}; }
 };
 
-// One position's row of the fixed-base comb: entries d = 0..128, PV_BCOMB_STRIDE words each.
+// One position's row of the fixed-base comb: entries d = 0..32768, PV_BCOMB_STRIDE words each.
 struct DevBRow {
     const uint4* r;
     __device__ __forceinline__ void load_part(int d, int part, uint32_t w[20]) const {
@@ -390,7 +391,7 @@ struct DevBRow {
 struct DevBRows {
     const uint4* base;
     __device__ __forceinline__ DevBRow row(int i) const {
-        return DevBRow{base + (uint32_t)i * PV_COMB_ENT * (PV_BCOMB_STRIDE / 4)};
+        return DevBRow{base + (uint32_t)i * PV_BCOMB_ENT * (PV_BCOMB_STRIDE / 4)};
     }
 };
 
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
     kw.req_key[i] = kw.slot_id[kw.req_key[i]];
     uint32_t ek[8], fs[8];
     sc_recode256(ek, k);
-    sc_recode256(fs, in.S);
+    sc_recode65536(fs, in.S);
     const uint32_t S = (uint32_t)wk.stride;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -744,8 +745,16 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * 160), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
-        std::vector<uint32_t> bc((size_t)PV_COMB_POS * PV_COMB_ENT * PV_BCOMB_STRIDE);
-        pv_build_b_comb(bc.data());
+        std::vector<uint32_t> bc((size_t)PV_BCOMB_POS * PV_BCOMB_ENT * PV_BCOMB_STRIDE);
+        {
+            ge_p3 base[PV_BCOMB_POS];
+            pv_bcomb_bases(base);
+            std::vector<std::thread> th;
+            for (int j = 0; j < PV_BCOMB_POS; j++)
+                th.emplace_back(pv_bcomb_build_position, bc.data() + (size_t)j * PV_BCOMB_ENT * PV_BCOMB_STRIDE,
+                                std::cref(base[j]));
+            for (auto& t : th) t.join();
+        }
         PV_HIP(hipMalloc((void**)&g_ctx.d_bcomb, bc.size() * 4), PV_ERR_ALLOC);
         PV_HIP(hipMemcpy(g_ctx.d_bcomb, bc.data(), bc.size() * 4, hipMemcpyHostToDevice), PV_ERR_ALLOC);
     }

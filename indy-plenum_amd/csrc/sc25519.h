@@ -149,3 +149,23 @@ PV_HD void sc_recode256(uint32_t out[8], const uint32_t a[8]) {
         out[w] = word;
     }
 }
+
+// Signed radix-65536 digits of a < 2^253: e_i in [-32768, 32767] for i < 15, e_15 in [0, 2^13].
+// Packed as 16-bit two's complement halfwords, digit i at bits [16i, 16i+16) of out[0..8).
+PV_HD void sc_recode65536(uint32_t out[8], const uint32_t a[8]) {
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const uint32_t h = (a[w] >> (16 * j)) & 0xFFFFu;
+            const uint32_t v = h + carry;
+            const bool last = (w == 7 && j == 1);
+            carry = last ? 0u : ((v + 0x8000u) >> 16);
+            const uint32_t e = v - (carry << 16);
+            word |= (e & 0xFFFFu) << (16 * j);
+        }
+        out[w] = word;
+    }
+}

@@ -105,6 +105,7 @@ PV_HD void pv_build_a_table(ATab& tab, const ge_p3& negA) {
 // Signed digit i of the packed recodings: nibble i of ek (radix 16), byte i of fs (radix 256).
 PV_HD int pv_nibble(uint32_t word, int i) { return ((int32_t)(word << (28 - 4 * (i & 7)))) >> 28; }
 PV_HD int pv_byte(uint32_t word, int i) { return ((int32_t)(word << (24 - 8 * (i & 3)))) >> 24; }
+PV_HD int pv_half(uint32_t word, int i) { return ((int32_t)(word << (16 - 16 * (i & 1)))) >> 16; }
 
 // A-table lookups come in two halves so that only 20 words of the entry are live at a time:
 // half 0 = (Y+X, Y-X), half 1 = (2Z, 2dT) of [|e|](-A); negative digits swap Y+X / Y-X and negate

@@ -7,6 +7,7 @@
 #include "comb.h"
 #include <string.h>
 #include <vector>
+#include <thread>
 
 extern "C" {
 
@@ -116,7 +117,7 @@ struct HostBRow {
 };
 struct HostBRows {
     const uint32_t* base;
-    HostBRow row(int i) const { return HostBRow{base + (size_t)i * PV_COMB_ENT * PV_BCOMB_STRIDE}; }
+    HostBRow row(int i) const { return HostBRow{base + (size_t)i * PV_BCOMB_ENT * PV_BCOMB_STRIDE}; }
 };
 
 // crypto_sign_open through the comb path: key expansion (chain + all fill blocks), radix-256
@@ -124,8 +125,14 @@ struct HostBRows {
 int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     static std::vector<uint32_t> bcomb;
     if (bcomb.empty()) {
-        bcomb.resize((size_t)PV_COMB_POS * PV_COMB_ENT * PV_BCOMB_STRIDE);
-        pv_build_b_comb(bcomb.data());
+        bcomb.resize((size_t)PV_BCOMB_POS * PV_BCOMB_ENT * PV_BCOMB_STRIDE);
+        ge_p3 base[PV_BCOMB_POS];
+        pv_bcomb_bases(base);
+        std::vector<std::thread> th;
+        for (int j = 0; j < PV_BCOMB_POS; j++)
+            th.emplace_back(pv_bcomb_build_position, bcomb.data() + (size_t)j * PV_BCOMB_ENT * PV_BCOMB_STRIDE,
+                            std::cref(base[j]));
+        for (auto& t : th) t.join();
     }
     std::vector<uint8_t> buf(smlen + 80, 0);
     memcpy(buf.data(), sm, smlen);
@@ -147,7 +154,7 @@ int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
             pv_comb_fill_block(HostCombRow{ctab.data() + (size_t)pos * PV_COMB_ENT * 40}, bases[pos], b);
     pv_dig_regs dig;
     sc_recode256(dig.e, k);
-    sc_recode256(dig.f, in.S);
+    sc_recode65536(dig.f, in.S);
     fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
     bool use[PV_ENC_BATCH];
     pv_comb_xyz(X[0], Y[0], Z[0], HostCombRows{ctab.data()}, HostBRows{bcomb.data()}, dig);

@@ -21,7 +21,7 @@ A10 = ctypes.c_uint32 * 10
 
 def build_hostcheck():
     src = os.path.join(HERE, "native", "hostcheck.hip")
-    cmd = ["/opt/rocm/bin/hipcc", "-O2", "-fPIC", "-shared", "--offload-arch=gfx950", "--offload-host-only",
+    cmd = ["/opt/rocm/bin/hipcc", "-O2", "-fPIC", "-shared", "-pthread", "--offload-arch=gfx950", "--offload-host-only",
            "-I" + os.path.join(ROOT, "indy-plenum_amd", "csrc"), src, "-o", LIB]
     subprocess.check_call(cmd)
 
