@@ -1,9 +1,14 @@
-// SHA-512 compression (FIPS 180-4) for the per-request hash k = SHA-512(R || A || M).
-// 64-bit words are split by the compiler into 32-bit halves; rotations lower to v_alignbit_b32.
+// SHA-512 (FIPS 180-4) for the per-request hash k = SHA-512(R || A || M) of the verify kernels.
+//
+// 64-bit words live in VGPR pairs: additions are single v_lshl_add_u64, every rotation is two
+// v_alignbit_b32 (a funnel shift of the two halves), Ch / Maj / the three-way XORs map to
+// v_bfi_b32 / v_xor_b32, byte swaps to v_perm_b32. Rounds are unrolled 16 at a time with the
+// message schedule in a static 16-word ring and the working variables rotated by renaming, so no
+// register moves or indexed register accesses remain (~34 VALU instructions per round).
+// Replaces libsodium's crypto_hash_sha512 inside crypto_sign_open (reached from the reference via
+// stp_core/crypto/nacl_wrappers.py:108).
 #pragma once
 #include "fe25519.h"
-
-#define PV_ROR64(x, n) (((x) >> (n)) | ((x) << (64 - (n))))
 
 static constexpr uint64_t PV_K512[80] = {
     0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
@@ -27,6 +32,42 @@ static constexpr uint64_t PV_K512[80] = {
     0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
     0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
+// ((hi:lo) >> s) mod 2^32 for 0 <= s < 32: one v_alignbit_b32
+PV_HD uint32_t pv_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
+
+PV_HD uint64_t pv_pack64(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
+
+// rotate right by a compile-time n (0 < n < 64, n != 32)
+template <int N>
+PV_HD uint64_t pv_rotr64(uint64_t x) {
+    const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
+    if (N < 32) return pv_pack64(pv_alignbit(lo, hi, N), pv_alignbit(hi, lo, N));
+    return pv_pack64(pv_alignbit(hi, lo, N - 32), pv_alignbit(lo, hi, N - 32));
+}
+template <int N>
+PV_HD uint64_t pv_shr64(uint64_t x) {
+    const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
+    return pv_pack64(hi >> N, pv_alignbit(hi, lo, N));
+}
+
+PV_HD uint32_t pv_bswap32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(0u, x, 0x00010203u);
+#else
+    return __builtin_bswap32(x);
+#endif
+}
+// byte-reverse a 64-bit word
+PV_HD uint64_t pv_bswap64(uint64_t x) {
+    return pv_pack64(pv_bswap32((uint32_t)x), pv_bswap32((uint32_t)(x >> 32)));
+}
+
 PV_HD void sha512_init(uint64_t st[8]) {
     st[0] = 0x6a09e667f3bcc908ULL; st[1] = 0xbb67ae8584caa73bULL;
     st[2] = 0x3c6ef372fe94f82bULL; st[3] = 0xa54ff53a5f1d36f1ULL;
@@ -34,36 +75,48 @@ PV_HD void sha512_init(uint64_t st[8]) {
     st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
 }
 
+// One round: the eight working variables rotate by renaming (the caller passes them shifted).
+#define PV_SHA_ROUND(a, b, c, d, e, f, g, h, kw)                                                   \
+    do {                                                                                          \
+        const uint64_t S1 = pv_rotr64<14>(e) ^ pv_rotr64<18>(e) ^ pv_rotr64<41>(e);               \
+        const uint64_t ch = g ^ (e & (f ^ g));                                                    \
+        const uint64_t t1 = h + S1 + ch + (kw);                                                   \
+        const uint64_t S0 = pv_rotr64<28>(a) ^ pv_rotr64<34>(a) ^ pv_rotr64<39>(a);               \
+        const uint64_t mj = (a & b) | (c & (a | b));                                              \
+        d += t1;                                                                                  \
+        h = t1 + S0 + mj;                                                                         \
+    } while (0)
+
 // One compression of a 128-byte block given as 16 big-endian words (already byte-swapped).
 PV_HD void sha512_compress(uint64_t st[8], const uint64_t blk[16]) {
     uint64_t w[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) w[i] = blk[i];
     uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll 16
-    for (int i = 0; i < 80; i++) {
-        uint64_t wi;
-        if (i < 16) {
-            wi = w[i & 15];
-        } else {
-            const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-            const uint64_t s0 = PV_ROR64(w15, 1) ^ PV_ROR64(w15, 8) ^ (w15 >> 7);
-            const uint64_t s1 = PV_ROR64(w2, 19) ^ PV_ROR64(w2, 61) ^ (w2 >> 6);
-            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-            w[i & 15] = wi;
+#pragma unroll 1
+    for (int r = 0; r < 80; r += 16) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int i = r + j;
+            if (r > 0) {
+                const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+                const uint64_t s0 = pv_rotr64<1>(w15) ^ pv_rotr64<8>(w15) ^ pv_shr64<7>(w15);
+                const uint64_t s1 = pv_rotr64<19>(w2) ^ pv_rotr64<61>(w2) ^ pv_shr64<6>(w2);
+                w[i & 15] += s0 + w[(i - 7) & 15] + s1;
+            }
+            const uint64_t kw = PV_K512[i] + w[i & 15];
+            switch (j & 7) {
+                case 0: PV_SHA_ROUND(a, b, c, d, e, f, g, h, kw); break;
+                case 1: PV_SHA_ROUND(h, a, b, c, d, e, f, g, kw); break;
+                case 2: PV_SHA_ROUND(g, h, a, b, c, d, e, f, kw); break;
+                case 3: PV_SHA_ROUND(f, g, h, a, b, c, d, e, kw); break;
+                case 4: PV_SHA_ROUND(e, f, g, h, a, b, c, d, kw); break;
+                case 5: PV_SHA_ROUND(d, e, f, g, h, a, b, c, kw); break;
+                case 6: PV_SHA_ROUND(c, d, e, f, g, h, a, b, kw); break;
+                default: PV_SHA_ROUND(b, c, d, e, f, g, h, a, kw); break;
+            }
         }
-        const uint64_t S1 = PV_ROR64(e, 14) ^ PV_ROR64(e, 18) ^ PV_ROR64(e, 41);
-        const uint64_t ch = g ^ (e & (f ^ g));
-        const uint64_t t1 = h + S1 + ch + PV_K512[i] + wi;
-        const uint64_t S0 = PV_ROR64(a, 28) ^ PV_ROR64(a, 34) ^ PV_ROR64(a, 39);
-        const uint64_t mj = (a & b) | (c & (a | b));
-        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
-
-PV_HD uint64_t pv_bswap64(uint64_t x) {
-    x = ((x & 0x00ff00ff00ff00ffULL) << 8) | ((x >> 8) & 0x00ff00ff00ff00ffULL);
-    x = ((x & 0x0000ffff0000ffffULL) << 16) | ((x >> 16) & 0x0000ffff0000ffffULL);
-    return (x << 32) | (x >> 32);
-}
+#undef PV_SHA_ROUND

@@ -280,33 +280,35 @@ PV_HD bool pv_key_ok_negate(ge_p3& negA, const uint32_t A[8]) {
     return ok;
 }
 
-// k = SHA-512(R || A || M) mod L.
+// k = SHA-512(R || A || M) mod L. The hash input is sm with bytes 32..63 (S) replaced by A, so
+// input word q >= 8 is sm word q; T = smlen bytes in total. Block assembly is branch-free: every
+// word is loaded (msgword may read up to 152 bytes past the record: PV_BLOB_SLACK covers it), then
+// masked / padded arithmetically, so lanes with different lengths never diverge inside a block.
 template <class MsgWord>
 PV_HD void pv_hash_k(uint32_t k[8], const pv_sig_words& in, uint64_t smlen, const MsgWord& msgword) {
-    // SHA-512 over R || A || M: the input is sm with bytes 32..63 (S) replaced by A, so SHA word
-    // q >= 8 is sm word q; T = smlen bytes in total.
-    const uint64_t T = smlen;
+    const uint32_t T = (uint32_t)smlen;
     uint64_t st[8];
     sha512_init(st);
-    const uint64_t nblocks = (T + 17 + 127) / 128;
-    for (uint64_t b = 0; b < nblocks; b++) {
+    const uint32_t nblocks = (T + 17 + 127) / 128;
+    for (uint32_t b = 0; b < nblocks; b++) {
         uint64_t blk[16];
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            const uint64_t q = 16 * b + j;
-            uint64_t raw;  // little-endian bytes 8q..8q+7 of the SHA input
-            if (q < 4) raw = ((uint64_t)in.R[2 * q + 1] << 32) | in.R[2 * q];
-            else if (q < 8) raw = ((uint64_t)in.A[2 * (q - 4) + 1] << 32) | in.A[2 * (q - 4)];
-            else raw = (8 * q < T) ? msgword(q) : 0;
-            const uint64_t pos = 8 * q;
-            if (pos + 8 > T) {
-                // bytes at or beyond T: keep the data bytes, then 0x80, then zeros
-                const uint64_t nb = (pos >= T) ? 0 : T - pos;  // data bytes in this word (0..7)
-                raw = (nb == 0) ? 0 : (raw & ((1ULL << (8 * nb)) - 1));
-                if (pos <= T) raw |= 0x80ULL << (8 * nb);
+            const uint32_t q = 16 * b + j;
+            uint64_t raw = msgword(q);  // little-endian bytes 8q..8q+7 of sm
+            if (j < 8) {                // block 0 only: R || A
+                const uint64_t ra = j < 4 ? pv_pack64(in.R[2 * j + 1], in.R[2 * j])
+                                          : pv_pack64(in.A[2 * (j - 4) + 1], in.A[2 * (j - 4)]);
+                raw = (b == 0) ? ra : raw;
             }
+            // bytes at or beyond T: 0x80, then zeros
+            const int32_t rem = (int32_t)T - (int32_t)(8 * q);
+            const uint32_t nb = rem < 0 ? 0u : (rem > 8 ? 8u : (uint32_t)rem);
+            const uint64_t mask = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+            const uint64_t pad = (rem >= 0 && rem < 8) ? (0x80ull << (8 * rem)) : 0ull;
+            raw = (raw & mask) | pad;
             uint64_t be = pv_bswap64(raw);
-            if (b == nblocks - 1 && j == 15) be = T * 8;  // bit length (upper 64 bits are zero)
+            if (j == 15 && b == nblocks - 1) be = (uint64_t)T * 8;  // bit length (upper 64 bits zero)
             blk[j] = be;
         }
         sha512_compress(st, blk);

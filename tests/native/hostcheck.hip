@@ -59,11 +59,11 @@ struct HostMsg {
 };
 
 // Full pipeline on the host: crypto_sign_open(sm, smlen, pk) == 0 ? 1 : 0.
-// sm must be readable for smlen + 8 bytes (the kernel contract: record slack).
+// sm is copied into a buffer with PV_BLOB_SLACK bytes of zero slack (the kernel contract).
 int hc_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     static std::vector<uint32_t> btab;
     if (btab.empty()) { btab.resize(PV_BTAB_ENTRIES * PV_BTAB_STRIDE); pv_build_b_table(btab.data()); }
-    std::vector<uint8_t> buf(smlen + 80, 0);
+    std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK
     memcpy(buf.data(), sm, smlen);
     pv_sig_words in;
     memcpy(in.R, buf.data(), 32);
@@ -134,7 +134,7 @@ int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
                             std::cref(base[j]));
         for (auto& t : th) t.join();
     }
-    std::vector<uint8_t> buf(smlen + 80, 0);
+    std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK
     memcpy(buf.data(), sm, smlen);
     pv_sig_words in;
     memcpy(in.R, buf.data(), 32);
@@ -167,7 +167,7 @@ int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
 
 // k = SHA-512(R||A||M) mod L through pv_prepare (exposes the hashing + reduction)
 void hc_prepare_k(uint8_t* kout, const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
-    std::vector<uint8_t> buf(smlen + 80, 0);
+    std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK
     memcpy(buf.data(), sm, smlen);
     pv_sig_words in; memcpy(in.R, buf.data(), 32); memcpy(in.S, buf.data() + 32, 32); memcpy(in.A, pk, 32);
     ge_p3 negA; uint32_t k[8]; HostMsg mw{buf.data()};
