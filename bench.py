@@ -228,7 +228,7 @@ def main():
     achieved = mac_kernel * n / (msm_avg_ms * 1e-3)
     pipeline_ms = sum(stage_ms.values())
     per_gpu_rate = n / (pipeline_ms * 1e-3)
-    mac_executed = (BC.MAC_COMB_MSM_KERNEL + BC.MAC_ENCODE / 4 + BC.MAC_COMB_PER_KEY * nkeys / n) if comb \
+    mac_executed = (BC.MAC_COMB_MSM + BC.MAC_ENCODE / 4 + BC.MAC_COMB_PER_KEY * nkeys / n) if comb \
         else (BC.MAC_PER_VERIFY - BC.MAC_ENCODE * 3 / 4)
 
     result = {
@@ -241,10 +241,10 @@ def main():
                    "record_bytes_avg": round(float(blob.nbytes) / n, 1),
                    "path": "keyed comb (%d distinct keys, tables built inside every step)" % nkeys if comb
                    else "per-request Straus"},
-        "roofline": {"bound": "valu", "kernel": "pv_comb_msm_kernel" if comb else "pv_msm_kernel",
+        "roofline": {"bound": "valu", "kernel": "pv_comb_a_kernel" if comb else "pv_msm_kernel",
                      "achieved": round(achieved / 1e12, 3), "peak": round(BC.PEAK_MAC_PER_S / 1e12, 3),
                      "unit": "TMAC/s (v_mad_u64_u32 int32 MACs)", "frac": round(achieved / BC.PEAK_MAC_PER_S, 4),
-                     "traffic": pmc_traffic("pv_comb_msm_kernel" if comb else "pv_msm_kernel"),
+                     "traffic": pmc_traffic("pv_comb_a_kernel" if comb else "pv_msm_kernel"),
                      "algorithmic_mac_per_verify": round(mac_kernel), "launch_ms": round(msm_avg_ms, 4)},
         "pipeline": {**{s + "_ms": round(v, 4) for s, v in stage_ms.items()},
                      "kernel_verifies_per_s_per_gpu": round(per_gpu_rate, 1),

@@ -47,7 +47,11 @@ MAC_MSM_KERNEL = MAC_LOOP
 # verdict: per request 32 cached-form additions of radix-256 T_A entries (4 M + 4 M to extended) and
 # 16 affine-niels additions of radix-65536 T_B entries (3 M + 4 M), the last one to projective
 # (3 M): no doublings. Its kernel's roofline uses its own algorithmic work, counted the same way:
-MAC_COMB_MSM_KERNEL = MAC_PER_MUL * (32 * 8 + 16 * 7 - 1)
+MAC_COMB_MSM = MAC_PER_MUL * (32 * 8 + 16 * 7 - 1)
+# it runs as two kernels: pv_comb_b_kernel ([S]B, 16 niels additions) overlapped with the per-key
+# table build, then pv_comb_a_kernel (the 32 T_A additions, the MSM stage and the roofline kernel)
+MAC_COMB_B_KERNEL = MAC_PER_MUL * 16 * 7
+MAC_COMB_MSM_KERNEL = MAC_PER_MUL * (32 * 8 - 1)
 # per distinct key (amortised over the requests that share it): decompression + 31 x 8 doublings
 # (4 S + 3 M, the last of each 8 to extended: +1 M) + 32 x 129 table entries (8 M + 1 M each)
 MAC_COMB_PER_KEY = _mac(_S_DECOMP, _M_DECOMP) + _mac(31 * 8 * 4, 31 * (8 * 3 + 1)) + MAC_PER_MUL * 32 * 129 * 9

@@ -81,8 +81,10 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
  *   KEYS    per-batch key deduplication and per-key expansion (keyed comb path only)
  *   PREP    per-request checks, SHA-512, reduction mod L, recoding (and decompression of A on the
  *           Straus path)
- *   TABLE   per-request [j](-A) multiples (Straus path) / per-key comb tables (comb path)
- *   MSM     the double-scalar multiplication [S]B + [k](-A) to projective coordinates
+ *   TABLE   per-request [j](-A) multiples (Straus path) / comb path: [S]B from the fixed-base comb
+ *           while the per-key comb tables are built on a second stream, then the join
+ *   MSM     the double-scalar multiplication [S]B + [k](-A) to projective coordinates (comb path:
+ *           the [k](-A) half, 32 table additions)
  *   ENCODE  batched inversion, canonical encoding, compare with R, verdict bits
  * and the number of launches (chunks). pv_kernel_times is the coarse three-way view
  * (KEYS+PREP, TABLE, MSM+ENCODE). pv_set_timing(0) stops recording. */

@@ -121,33 +121,47 @@ PV_HD void pv_comb_add_cached(ge_p1p1& r, const ge_p3& p, const Entry& ent, int 
     fe_sub(r.T, d, c);
 }
 
-// Q = [S]B + [k](-A) from the comb tables: arows.row(i) / brows.row(j) give the A row of radix-256
-// position i and the B row of radix-65536 position j (objects with load_half / load_part); dig holds
-// the packed digits (ek: 4 signed bytes of k per word, fs: 2 signed halfwords of S per word).
+// The two halves of a comb verification, split so that [S]B (which needs only the fixed-base table)
+// can run while the per-key tables are still being built:
+//   pv_comb_b_acc:  acc = [S]B = sum_j T_B[j][f_j]          16 niels additions, extended result
+//   pv_comb_a_xyz:  Q = acc + sum_i T_A[i][e_i]              32 cached additions, projective result
+// arows.row(i) / brows.row(j) give the A row of radix-256 position i and the B row of radix-65536
+// position j (objects with load_half / load_part); dig holds the packed digits (ek: 4 signed bytes
+// of k per word, fs: 2 signed halfwords of S per word).
+template <class BRows, class Dig>
+PV_HD void pv_comb_b_acc(ge_p3& acc, const BRows& brows, const Dig& dig) {
+    ge_p3_identity(acc);
+    ge_p1p1 t;
+    uint32_t fw = 0;
+    for (int j = PV_BCOMB_POS - 1; j >= 0; j--) {
+        if ((j & 1) == 1) fw = dig.fs(j >> 1);
+        pv_add_b(t, acc, brows.row(j), pv_half(fw, j));
+        ge_niels_p1p1_to_p3(acc, t);
+    }
+}
+
+template <class ARows, class Dig>
+PV_HD void pv_comb_a_xyz(fe& X, fe& Y, fe& Z, const ge_p3& accB, const ARows& arows, const Dig& dig) {
+    ge_p3 acc = accB;
+    ge_p1p1 t;
+    uint32_t ew = 0;
+    for (int i = PV_COMB_POS - 1; i >= 0; i--) {
+        if ((i & 3) == 3) ew = dig.ek(i >> 2);
+        pv_comb_add_cached(t, acc, arows.row(i), pv_byte(ew, i));
+        if (i > 0) {
+            ge_p1p1_to_p3(acc, t);
+        } else {
+            ge_p1p1_to_p2(X, Y, Z, t);
+        }
+    }
+}
+
+// Q = [S]B + [k](-A) from the comb tables (both halves in one call: host tests).
 template <class ARows, class BRows, class Dig>
 PV_HD void pv_comb_xyz(fe& X, fe& Y, fe& Z, const ARows& arows, const BRows& brows, const Dig& dig) {
     ge_p3 acc;
-    ge_p3_identity(acc);
-    ge_p1p1 t;
-    uint32_t ew = 0, fw = 0;
-    for (int i = PV_COMB_POS - 1; i >= 0; i--) {
-        if ((i & 3) == 3) {
-            ew = dig.ek(i >> 2);
-            fw = dig.fs(i >> 2);
-        }
-        const int e = pv_byte(ew, i);
-        pv_comb_add_cached(t, acc, arows.row(i), e);
-        ge_p1p1_to_p3(acc, t);
-        if ((i & 1) == 0) {
-            const int f = pv_half(fw, i >> 1);
-            pv_add_b(t, acc, brows.row(i >> 1), f);
-            if (i > 0) {
-                ge_niels_p1p1_to_p3(acc, t);
-            } else {
-                ge_niels_p1p1_to_p2(X, Y, Z, t);
-            }
-        }
-    }
+    pv_comb_b_acc(acc, brows, dig);
+    pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
 }
 
 // ---------------------------------------------------------------- fixed-base comb (host, init)

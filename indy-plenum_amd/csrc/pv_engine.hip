@@ -25,6 +25,9 @@
 #include "../../include/plenum_verify.h"
 
 static constexpr int PV_BLOCK = 256;
+#ifndef PV_CHAIN_QUAD
+#define PV_CHAIN_QUAD 1  // four lanes per key in the per-key chain (pv_key_chain_quad_kernel)
+#endif
 #ifndef PV_MSM_MINBLOCKS
 #define PV_MSM_MINBLOCKS 2  // workgroups per CU the msm kernel's register budget is sized for
 #endif
@@ -124,7 +127,8 @@ struct DevMsg {
 //   atab  [9 entries][10 quads][n] uint4   cached [j](-A), j = 0..8
 //   digits[16][n] uint32                    radix-16 digits of k (8 words), radix-256 of S (8 words)
 //   flags [n] uint32                        1 = every libsodium pre-check passed
-//   q     [30][n] uint32                    projective Q = (X, Y, Z) from the msm kernel
+//   q     [40][n] uint32                    projective Q = (X, Y, Z) from the msm kernel (rows 0..29);
+//                                           the comb path's [S]B half parks an extended point here
 struct Work {
     uint4* atab;
     uint32_t* digits;
@@ -399,6 +403,7 @@ struct DevBRows {
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
                                                                     Gate gate) {
     if (!gate.comb()) return;
+    __builtin_amdgcn_s_setprio(3);
     const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;
     if (id >= *kw.nkeys) return;
     uint32_t A[8];
@@ -407,6 +412,102 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_kernel(const uint8_t
     const bool ok = pv_key_ok_negate(negA, A);
     kw.key_flag[id] = ok ? 1u : 0u;
     pv_comb_chain(DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * 10}, negA);
+}
+
+// ---- quad-cooperative key chain: four lanes per key shorten the per-key critical path ~2x.
+// The chain of 248 doublings is the only long dependency of the comb path and it runs on very few
+// lanes (one per distinct key), so its LATENCY, not its work, is what the batch waits for. Each
+// doubling's four squarings (X^2, Y^2, Z^2, (X+Y)^2) run on the four lanes of a quad at once and
+// so do its three (or four) products; quad_perm DPP broadcasts exchange the results.
+__device__ __forceinline__ uint32_t pv_quad_bcast(uint32_t v, int r) {
+    switch (r) {
+        case 0: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);
+        case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x55, 0xF, 0xF, false);
+        case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, false);
+        default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xF, 0xF, false);
+    }
+}
+__device__ __forceinline__ void pv_fe_bcast(fe& h, const fe& f, int r) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) h.v[i] = pv_quad_bcast(f.v[i], r);
+}
+// h = (role == 0) ? a : (role == 1) ? b : (role == 2) ? c : d, branch-free: the role masks are
+// opaque to the compiler (see pv_key_chain_quad_kernel), so it selects per lane with v_cndmask
+// instead of specialising the field arithmetic per role into divergent copies.
+struct QuadRole {
+    uint32_t m0, m1, m2;  // all-ones iff role == 0 / 1 / 2
+};
+__device__ __forceinline__ void pv_fe_sel4(fe& h, const fe& a, const fe& b, const fe& c, const fe& d,
+                                           const QuadRole& q) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const uint32_t cd = q.m2 ? c.v[i] : d.v[i];
+        const uint32_t bcd = q.m1 ? b.v[i] : cd;
+        h.v[i] = q.m0 ? a.v[i] : bcd;
+    }
+}
+
+// One doubling of (X : Y : Z) (ge_p2_dbl + ge_p1p1_to_p2/p3), quad-parallel; T is produced when
+// want_t (it is the fourth lane's product).
+__device__ __forceinline__ void pv_quad_dbl(fe& X, fe& Y, fe& Z, fe& T, const QuadRole& role, bool want_t) {
+    fe in, s, XX, YY, ZZ, S, t;
+    fe_add(t, X, Y);
+    pv_fe_sel4(in, X, Y, Z, t, role);
+    fe_sq(s, in);
+    pv_fe_bcast(XX, s, 0);
+    pv_fe_bcast(YY, s, 1);
+    pv_fe_bcast(ZZ, s, 2);
+    pv_fe_bcast(S, s, 3);
+    ge_p1p1 r;
+    fe_add(r.Y, YY, XX);
+    fe_sub(r.Z, YY, XX);
+    fe_sub4p(r.X, S, r.Y);
+    fe_add(t, ZZ, ZZ);
+    fe_sub4p(t, t, r.Z);
+    fe_carry(r.T, t);
+    // lane 0: X = rX rT, 1: Y = rY rZ, 2: Z = rZ rT, 3: T = rX rY (f side may be uncarried rX)
+    fe f, g, o;
+    pv_fe_sel4(f, r.X, r.Y, r.Z, r.X, role);
+    pv_fe_sel4(g, r.T, r.Z, r.T, r.Y, role);
+    fe_mul(o, f, g);
+    pv_fe_bcast(X, o, 0);
+    pv_fe_bcast(Y, o, 1);
+    pv_fe_bcast(Z, o, 2);
+    if (want_t) pv_fe_bcast(T, o, 3);
+}
+
+// Per distinct key, four lanes: libsodium's key checks, -A, and the bases [256^i](-A), i = 0..31.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
+                                                                         Gate gate) {
+    if (!gate.comb()) return;
+    // the chain is the batch's critical path and shares SIMDs with the per-request prep kernel:
+    // take issue priority over it
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
+    const uint32_t nk = *kw.nkeys;
+    const uint32_t id = g >> 2;
+    uint32_t rl = g & 3;
+    asm volatile("" : "+v"(rl));  // opaque: keep the per-role selects branch-free
+    const QuadRole role{rl == 0 ? ~0u : 0u, rl == 1 ? ~0u : 0u, rl == 2 ? ~0u : 0u};
+    // whole quads exit together (nk is uniform), so the DPP partners of a live lane are live
+    if (id >= nk) return;
+    uint32_t A[8];
+    pv_load_pk(A, pk, kw.key_owner[id]);
+    ge_p3 cur;
+    const bool ok = pv_key_ok_negate(cur, A);
+    if (rl == 0) kw.key_flag[id] = ok ? 1u : 0u;
+    uint32_t* b = reinterpret_cast<uint32_t*>(kw.bases + (uint64_t)id * PV_COMB_POS * 10);
+    fe X = cur.X, Y = cur.Y, Z = cur.Z, T = cur.T;
+    for (int i = 0; i < PV_COMB_POS; i++) {
+        if (i > 0) {
+            for (int j = 0; j < 8; j++) pv_quad_dbl(X, Y, Z, T, role, j == 7);
+        }
+        // lane r stores component r (X, Y, Z, T) of base i: words 10 r .. 10 r + 9
+        fe mine;
+        pv_fe_sel4(mine, X, Y, Z, T, role);
+#pragma unroll
+        for (int q = 0; q < 10; q++) b[i * 40 + 10 * rl + q] = mine.v[q];
+    }
 }
 
 // Per (key, position, block of 16 entries): the comb table rows. Grid-stride over nkeys * 256 items.
@@ -460,29 +561,54 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
     wk.flags[i] = ok ? 1u : 0u;
 }
 
-// Per request on the comb path: Q = sum of 32 T_A and 32 T_B entries (no doublings).
-__global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_comb_msm_kernel(uint64_t n, Work wk, KeyWork kw,
-                                                                                 const uint4* __restrict__ bcomb,
-                                                                                 Gate gate) {
+// Per request on the comb path, first half: acc = [S]B from the fixed-base comb (16 additions).
+// Needs no per-key data, so it runs on the main stream while the key stream builds the tables.
+// acc (extended, 40 words) goes to q rows 0..39.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
+                                                                 Gate gate) {
     if (!gate.comb()) return;
-    const uint32_t i0 = blockIdx.x * PV_BLOCK + threadIdx.x;
-    const bool active = i0 < n;
-    const uint32_t i = active ? i0 : (uint32_t)n - 1;
-    const uint32_t id = kw.req_key[i];
-    const DevCombRows arows{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10};
-    const DevBRows brows{bcomb};
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
-    fe X, Y, Z;
-    pv_comb_xyz(X, Y, Z, arows, brows, dig);
-    if (active) {
-        const uint32_t S = (uint32_t)wk.stride;
-        if (kw.key_flag[id] == 0) wk.flags[i] = 0;
+    ge_p3 acc;
+    pv_comb_b_acc(acc, DevBRows{bcomb}, dig);
+    const uint32_t S = (uint32_t)wk.stride;
 #pragma unroll
-        for (int q = 0; q < 10; q++) {
-            wk.q[q * S + i] = X.v[q];
-            wk.q[(10 + q) * S + i] = Y.v[q];
-            wk.q[(20 + q) * S + i] = Z.v[q];
-        }
+    for (int q = 0; q < 10; q++) {
+        wk.q[q * S + i] = acc.X.v[q];
+        wk.q[(10 + q) * S + i] = acc.Y.v[q];
+        wk.q[(20 + q) * S + i] = acc.Z.v[q];
+        wk.q[(30 + q) * S + i] = acc.T.v[q];
+    }
+}
+
+// Second half: Q = acc + [k](-A) from the key's comb table (32 additions, no doublings), projective
+// Q to q rows 0..29; the key's own libsodium checks are folded into flags[i] here.
+__global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
+                                                                               Gate gate) {
+    if (!gate.comb()) return;
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t id = kw.req_key[i];
+    const uint32_t S = (uint32_t)wk.stride;
+    ge_p3 acc;
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        acc.X.v[q] = wk.q[q * S + i];
+        acc.Y.v[q] = wk.q[(10 + q) * S + i];
+        acc.Z.v[q] = wk.q[(20 + q) * S + i];
+        acc.T.v[q] = wk.q[(30 + q) * S + i];
+    }
+    const DevCombRows arows{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10};
+    const DevDigits dig{wk.digits, S, i};
+    fe X, Y, Z;
+    pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
+    if (kw.key_flag[id] == 0) wk.flags[i] = 0;
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        wk.q[q * S + i] = X.v[q];
+        wk.q[(10 + q) * S + i] = Y.v[q];
+        wk.q[(20 + q) * S + i] = Z.v[q];
     }
 }
 
@@ -648,8 +774,13 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
             // overlapped with the per-request prep on the main stream
             PV_HIP(hipEventRecord(g_ctx.ev_keys_ready, stream), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(g_ctx.kstream, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
+#if PV_CHAIN_QUAD
+            hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK),
+                               0, g_ctx.kstream, d_pk + 32 * c0, kw, gate);
+#else
             hipLaunchKernelGGL(pv_key_chain_kernel, dim3((limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
                                g_ctx.kstream, d_pk + 32 * c0, kw, gate);
+#endif
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             const uint64_t items = (uint64_t)limit * PV_COMB_POS * PV_COMB_BLOCKS;
             const unsigned fgrid = (unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096);
@@ -669,14 +800,19 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
         if ((rc = mark(PV_STAGE_TABLE))) return rc;
         hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (limit > 0) PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
+        if (limit > 0) {
+            // [S]B while the key stream finishes the tables, then join
+            hipLaunchKernelGGL(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bcomb,
+                               gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
+        }
         if ((rc = mark(PV_STAGE_MSM))) return rc;
         hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                            g_ctx.d_btab, g_ctx.work, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         if (limit > 0) {
-            hipLaunchKernelGGL(pv_comb_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.kw,
-                               g_ctx.d_bcomb, gate);
+            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         }
         if ((rc = mark(PV_STAGE_ENCODE))) return rc;
@@ -730,7 +866,7 @@ int pv_init(int device) {
     PV_HIP(hipMalloc((void**)&g_ctx.work.atab, S * 9 * 160), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * 16 * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
-    PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 30 * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 40 * 4), PV_ERR_ALLOC);
     {
         KeyWork& kw = g_ctx.kw;
         const uint64_t H = 2 * S;
