@@ -613,34 +613,39 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_comb_a_kernel(u
 }
 
 // Kernel 3: encode Q for PV_ENC_BATCH requests per lane with one shared inversion, compare with R,
-// one __ballot per request group. Wave w covers requests [256 w, 256 w + 256): lane l handles
-// 256 w + l + 64 t, t = 0..3, so every load is coalesced and group t's ballot is verdict word 4 w + t.
+// one __ballot per request group. Wave w covers requests [64 B w, 64 B (w + 1)) (B = PV_ENC_BATCH):
+// lane l handles 64 B w + l + 64 t, t = 0..B-1, so every load is coalesced and group t's ballot is
+// verdict word B w + t. Points are re-read from q rather than held (B x 30 registers).
 static constexpr int PV_ENC_PER_WAVE = 64 * PV_ENC_BATCH;
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* __restrict__ sm,
-                                                                 const uint64_t* __restrict__ off, uint64_t n,
-                                                                 Work wk, uint64_t* __restrict__ verdict) {
-    const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
-    const uint32_t w = g >> 6, l = g & 63;
-    fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
-    bool use[PV_ENC_BATCH];
-    const uint32_t S = (uint32_t)wk.stride;
-#pragma unroll
-    for (int t = 0; t < PV_ENC_BATCH; t++) {
+struct DevEncSrc {
+    const uint32_t* q;
+    uint32_t S, w, l;
+    uint64_t n;
+    __device__ __forceinline__ uint32_t req(int t) const {
         const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
-        const bool in = r < n;
-        const uint32_t rr = in ? r : 0;
-#pragma unroll
-        for (int q = 0; q < 10; q++) {
-            X[t].v[q] = wk.q[q * S + rr];
-            Y[t].v[q] = wk.q[(10 + q) * S + rr];
-            Z[t].v[q] = wk.q[(20 + q) * S + rr];
-        }
-        use[t] = in && wk.flags[rr] != 0;
+        return r < n ? r : 0;
     }
-    uint32_t enc[PV_ENC_BATCH][8];
-    pv_encode_batch(enc, X, Y, Z, use);
+    __device__ __forceinline__ void z(int t, fe& o) const {
+        const uint32_t r = req(t);
 #pragma unroll
-    for (int t = 0; t < PV_ENC_BATCH; t++) {
+        for (int k = 0; k < 10; k++) o.v[k] = q[(20 + k) * S + r];
+    }
+    __device__ __forceinline__ void xy(int t, fe& x, fe& y) const {
+        const uint32_t r = req(t);
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            x.v[k] = q[k * S + r];
+            y.v[k] = q[(10 + k) * S + r];
+        }
+    }
+};
+struct DevEncSink {
+    const uint8_t* sm;
+    const uint64_t* off;
+    uint64_t* verdict;
+    uint32_t w, l;
+    uint64_t n;
+    __device__ __forceinline__ void operator()(int t, const uint32_t enc[8], bool use) const {
         const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
         const uint32_t rr = r < n ? r : 0;
         const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[rr]);
@@ -648,11 +653,25 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* _
         uint32_t R[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) R[q] = mw.dw(q);
-        const bool ok = use[t] && pv_words_equal(enc[t], R);
+        const bool ok = use && pv_words_equal(enc, R);
         const uint64_t bits = __ballot(ok);
         const uint32_t r0 = w * PV_ENC_PER_WAVE + 64 * t;
         if (l == 0 && r0 < n) verdict[r0 >> 6] = bits;
     }
+};
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* __restrict__ sm,
+                                                                 const uint64_t* __restrict__ off, uint64_t n,
+                                                                 Work wk, uint64_t* __restrict__ verdict) {
+    const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
+    const uint32_t w = g >> 6, l = g & 63;
+    const DevEncSrc src{wk.q, (uint32_t)wk.stride, w, l, n};
+    bool use[PV_ENC_BATCH];
+#pragma unroll
+    for (int t = 0; t < PV_ENC_BATCH; t++) {
+        const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
+        use[t] = r < n && wk.flags[r < n ? r : 0] != 0;
+    }
+    pv_encode_batch_stream(src, use, DevEncSink{sm, off, verdict, w, l, n});
 }
 
 // ------------------------------------------------------------------------------------------ host

@@ -216,18 +216,22 @@ PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const 
 // c_t = z_0 ... z_t, inv = c_last^-1, then z_t^-1 = inv * c_{t-1} and inv *= z_t going down.
 // A point whose use flag is clear (failed pre-checks, or Z = 0 on garbage input) contributes
 // z = 1 so it cannot poison the shared inverse; its encoding is then meaningless and the caller
-// masks its verdict.
-static constexpr int PV_ENC_BATCH = 4;
-PV_HD void pv_encode_batch(uint32_t out[PV_ENC_BATCH][8], const fe X[PV_ENC_BATCH], const fe Y[PV_ENC_BATCH],
-                           const fe Z[PV_ENC_BATCH], bool use[PV_ENC_BATCH]) {
-    fe z[PV_ENC_BATCH], c[PV_ENC_BATCH];
+// masks its verdict. `src` streams the points: src.z(t, Z) and src.xy(t, X, Y) may be called more
+// than once for the same t (the device reloads instead of holding 8 points in registers), and
+// sink(t, enc, use) receives each encoding in descending t.
+static constexpr int PV_ENC_BATCH = 8;
+template <class Src, class Sink>
+PV_HD void pv_encode_batch_stream(const Src& src, bool use[PV_ENC_BATCH], const Sink& sink) {
+    fe c[PV_ENC_BATCH];
 #pragma unroll
     for (int t = 0; t < PV_ENC_BATCH; t++) {
-        use[t] = use[t] && !fe_iszero(Z[t]);
-        fe_1(z[t]);
-        fe_cmov(z[t], Z[t], use[t]);
-        if (t == 0) fe_copy(c[0], z[0]);
-        else fe_mul(c[t], c[t - 1], z[t]);
+        fe Z, z;
+        src.z(t, Z);
+        use[t] = use[t] && !fe_iszero(Z);
+        fe_1(z);
+        fe_cmov(z, Z, use[t]);
+        if (t == 0) fe_copy(c[0], z);
+        else fe_mul(c[t], c[t - 1], z);
     }
     fe inv;
     fe_invert(inv, c[PV_ENC_BATCH - 1]);
@@ -235,17 +239,41 @@ PV_HD void pv_encode_batch(uint32_t out[PV_ENC_BATCH][8], const fe X[PV_ENC_BATC
     for (int t = PV_ENC_BATCH - 1; t >= 0; t--) {
         fe zi;
         if (t > 0) {
+            fe Z, z;
+            src.z(t, Z);
+            fe_1(z);
+            fe_cmov(z, Z, use[t]);
             fe_mul(zi, inv, c[t - 1]);
-            fe_mul(inv, inv, z[t]);
+            fe_mul(inv, inv, z);
         } else {
             fe_copy(zi, inv);
         }
-        fe x, y;
-        fe_mul(x, X[t], zi);
-        fe_mul(y, Y[t], zi);
-        fe_tobytes32(out[t], y);
-        out[t][7] ^= fe_isnegative(x) << 31;
+        fe X, Y, x, y;
+        src.xy(t, X, Y);
+        fe_mul(x, X, zi);
+        fe_mul(y, Y, zi);
+        uint32_t enc[8];
+        fe_tobytes32(enc, y);
+        enc[7] ^= fe_isnegative(x) << 31;
+        sink(t, enc, use[t]);
     }
+}
+
+// Array form (host tests).
+struct pv_enc_arrays {
+    const fe *X, *Y, *Z;
+    PV_HD void z(int t, fe& o) const { o = Z[t]; }
+    PV_HD void xy(int t, fe& x, fe& y) const { x = X[t]; y = Y[t]; }
+};
+struct pv_enc_out {
+    uint32_t (*out)[8];
+    PV_HD void operator()(int t, const uint32_t enc[8], bool) const {
+        for (int q = 0; q < 8; q++) out[t][q] = enc[q];
+    }
+};
+PV_HD void pv_encode_batch(uint32_t out[PV_ENC_BATCH][8], const fe X[PV_ENC_BATCH], const fe Y[PV_ENC_BATCH],
+                           const fe Z[PV_ENC_BATCH], bool use[PV_ENC_BATCH]) {
+    pv_encode_batch_stream(pv_enc_arrays{X, Y, Z}, use, pv_enc_out{out});
 }
 
 // Digit words held in registers (host tests and small callers).
