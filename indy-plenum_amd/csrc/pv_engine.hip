@@ -28,6 +28,9 @@ static constexpr int PV_BLOCK = 256;
 #ifndef PV_CHAIN_QUAD
 #define PV_CHAIN_QUAD 1  // four lanes per key in the per-key chain (pv_key_chain_quad_kernel)
 #endif
+#ifndef PV_COMB_A_MINBLOCKS
+#define PV_COMB_A_MINBLOCKS 3
+#endif
 #ifndef PV_MSM_MINBLOCKS
 #define PV_MSM_MINBLOCKS 2  // workgroups per CU the msm kernel's register budget is sized for
 #endif
@@ -36,6 +39,32 @@ static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tabl
 static constexpr uint32_t PV_COMB_MIN_REUSE = 16; // AUTO: comb path iff distinct keys <= requests / 16
 
 // ---------------------------------------------------------------------------------------- device
+
+// Row r of a [rows][S] structure-of-arrays buffer: a wave-uniform pointer (SGPRs), so each access
+// is one global_load/store with a 32-bit per-lane offset instead of a live 64-bit address per row.
+template <class T>
+__device__ __forceinline__ T* pv_row(T* base, uint32_t r, uint32_t S) {
+    return base + (size_t)r * S;
+}
+
+// [rows][S] u32 structure-of-arrays buffer through a buffer resource: every access is one
+// buffer_load/store_dword with the lane's 32-bit byte offset in a VGPR and the row offset in an
+// SGPR (soffset), so rows cost no per-lane address registers (global_load addressing kept 40 live
+// 64-bit addresses for a 40-row point).
+struct Soa {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t S4;  // row stride in bytes
+    __device__ __forceinline__ Soa(uint32_t* base, uint64_t rows, uint64_t S)
+        : r(__builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)(rows * S * 4 < 0x7fffffffull ? rows * S * 4 : 0x7fffffffull),
+                                              0x00020000)),
+          S4((uint32_t)(S * 4)) {}
+    __device__ __forceinline__ uint32_t ld(uint32_t row, uint32_t i) const {
+        return __builtin_amdgcn_raw_buffer_load_b32(r, i * 4, row * S4, 0);
+    }
+    __device__ __forceinline__ void st(uint32_t row, uint32_t i, uint32_t v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(v, r, i * 4, row * S4, 0);
+    }
+};
 
 // Per-lane cached table of [j](-A) in HBM, layout [entry][quad][slot] uint4. Indices are 32-bit
 // (chunk <= 2^20 slots, so (9 * 10 + 9) * 2^20 + slot < 2^32) so each access is a uniform 64-bit base
@@ -103,11 +132,12 @@ struct LdsBTab {
 // Digit words of k (radix 16, rows 0..7) and S (radix 256, rows 8..15), one coalesced load each time
 // the Straus loop enters a new group of 8 windows.
 struct DevDigits {
-    const uint32_t* base;
-    uint32_t stride;
+    Soa d;
     uint32_t slot;
-    __device__ __forceinline__ uint32_t ek(int q) const { return base[(uint32_t)q * stride + slot]; }
-    __device__ __forceinline__ uint32_t fs(int q) const { return base[(uint32_t)(8 + q) * stride + slot]; }
+    __device__ __forceinline__ DevDigits(uint32_t* base, uint32_t stride, uint32_t slot_)
+        : d(base, 16, stride), slot(slot_) {}
+    __device__ __forceinline__ uint32_t ek(int q) const { return d.ld(q, slot); }
+    __device__ __forceinline__ uint32_t fs(int q) const { return d.ld(8 + q, slot); }
 };
 
 // Request bytes at an arbitrary byte offset: aligned dword loads + v_alignbyte_b32 funnel shifts.
@@ -211,10 +241,11 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __r
     uint32_t ek[8], fs[8];
     sc_recode16(ek, k);
     sc_recode256(fs, in.S);
+    const Soa ds(wk.digits, 16, wk.stride);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-        wk.digits[(uint64_t)q * wk.stride + i] = ek[q];
-        wk.digits[(uint64_t)(8 + q) * wk.stride + i] = fs[q];
+        ds.st(q, (uint32_t)i, ek[q]);
+        ds.st(8 + q, (uint32_t)i, fs[q]);
     }
     wk.flags[i] = ok ? 1u : 0u;
 }
@@ -257,11 +288,12 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
     fe X, Y, Z;
     pv_straus_xyz(X, Y, Z, at, bt, dig);
     if (active) {
+        const Soa qs(wk.q, 40, wk.stride);
 #pragma unroll
         for (int q = 0; q < 10; q++) {
-            wk.q[(uint32_t)q * (uint32_t)wk.stride + (uint32_t)i] = X.v[q];
-            wk.q[(uint32_t)(10 + q) * (uint32_t)wk.stride + (uint32_t)i] = Y.v[q];
-            wk.q[(uint32_t)(20 + q) * (uint32_t)wk.stride + (uint32_t)i] = Z.v[q];
+            qs.st(q, (uint32_t)i, X.v[q]);
+            qs.st(10 + q, (uint32_t)i, Y.v[q]);
+            qs.st(20 + q, (uint32_t)i, Z.v[q]);
         }
     }
 }
@@ -552,11 +584,11 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
     uint32_t ek[8], fs[8];
     sc_recode256(ek, k);
     sc_recode65536(fs, in.S);
-    const uint32_t S = (uint32_t)wk.stride;
+    const Soa ds(wk.digits, 16, wk.stride);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-        wk.digits[q * S + i] = ek[q];
-        wk.digits[(8 + q) * S + i] = fs[q];
+        ds.st(q, i, ek[q]);
+        ds.st(8 + q, i, fs[q]);
     }
     wk.flags[i] = ok ? 1u : 0u;
 }
@@ -572,32 +604,33 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     ge_p3 acc;
     pv_comb_b_acc(acc, DevBRows{bcomb}, dig);
-    const uint32_t S = (uint32_t)wk.stride;
+    const Soa qs(wk.q, 40, wk.stride);
 #pragma unroll
     for (int q = 0; q < 10; q++) {
-        wk.q[q * S + i] = acc.X.v[q];
-        wk.q[(10 + q) * S + i] = acc.Y.v[q];
-        wk.q[(20 + q) * S + i] = acc.Z.v[q];
-        wk.q[(30 + q) * S + i] = acc.T.v[q];
+        qs.st(q, i, acc.X.v[q]);
+        qs.st(10 + q, i, acc.Y.v[q]);
+        qs.st(20 + q, i, acc.Z.v[q]);
+        qs.st(30 + q, i, acc.T.v[q]);
     }
 }
 
 // Second half: Q = acc + [k](-A) from the key's comb table (32 additions, no doublings), projective
 // Q to q rows 0..29; the key's own libsodium checks are folded into flags[i] here.
-__global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
+__global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                Gate gate) {
     if (!gate.comb()) return;
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t id = kw.req_key[i];
     const uint32_t S = (uint32_t)wk.stride;
+    const Soa qs(wk.q, 40, wk.stride);
     ge_p3 acc;
 #pragma unroll
     for (int q = 0; q < 10; q++) {
-        acc.X.v[q] = wk.q[q * S + i];
-        acc.Y.v[q] = wk.q[(10 + q) * S + i];
-        acc.Z.v[q] = wk.q[(20 + q) * S + i];
-        acc.T.v[q] = wk.q[(30 + q) * S + i];
+        acc.X.v[q] = qs.ld(q, i);
+        acc.Y.v[q] = qs.ld(10 + q, i);
+        acc.Z.v[q] = qs.ld(20 + q, i);
+        acc.T.v[q] = qs.ld(30 + q, i);
     }
     const DevCombRows arows{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10};
     const DevDigits dig{wk.digits, S, i};
@@ -606,9 +639,9 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_comb_a_kernel(u
     if (kw.key_flag[id] == 0) wk.flags[i] = 0;
 #pragma unroll
     for (int q = 0; q < 10; q++) {
-        wk.q[q * S + i] = X.v[q];
-        wk.q[(10 + q) * S + i] = Y.v[q];
-        wk.q[(20 + q) * S + i] = Z.v[q];
+        qs.st(q, i, X.v[q]);
+        qs.st(10 + q, i, Y.v[q]);
+        qs.st(20 + q, i, Z.v[q]);
     }
 }
 
@@ -618,8 +651,8 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_comb_a_kernel(u
 // verdict word B w + t. Points are re-read from q rather than held (B x 30 registers).
 static constexpr int PV_ENC_PER_WAVE = 64 * PV_ENC_BATCH;
 struct DevEncSrc {
-    const uint32_t* q;
-    uint32_t S, w, l;
+    Soa q;
+    uint32_t w, l;
     uint64_t n;
     __device__ __forceinline__ uint32_t req(int t) const {
         const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
@@ -628,14 +661,14 @@ struct DevEncSrc {
     __device__ __forceinline__ void z(int t, fe& o) const {
         const uint32_t r = req(t);
 #pragma unroll
-        for (int k = 0; k < 10; k++) o.v[k] = q[(20 + k) * S + r];
+        for (int k = 0; k < 10; k++) o.v[k] = q.ld(20 + k, r);
     }
     __device__ __forceinline__ void xy(int t, fe& x, fe& y) const {
         const uint32_t r = req(t);
 #pragma unroll
         for (int k = 0; k < 10; k++) {
-            x.v[k] = q[k * S + r];
-            y.v[k] = q[(10 + k) * S + r];
+            x.v[k] = q.ld(k, r);
+            y.v[k] = q.ld(10 + k, r);
         }
     }
 };
@@ -664,7 +697,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* _
                                                                  Work wk, uint64_t* __restrict__ verdict) {
     const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t w = g >> 6, l = g & 63;
-    const DevEncSrc src{wk.q, (uint32_t)wk.stride, w, l, n};
+    const DevEncSrc src{Soa(wk.q, 40, wk.stride), w, l, n};
     bool use[PV_ENC_BATCH];
 #pragma unroll
     for (int t = 0; t < PV_ENC_BATCH; t++) {
