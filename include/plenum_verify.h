@@ -100,8 +100,9 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
  *   PV_PATH_COMB    per batch: deduplicate keys; per DISTINCT key: decompress and expand a
  *                   radix-256 comb table; per request: 64 table additions, no doublings
  *                   (falls back to Straus when a chunk has more distinct keys than the tables hold)
- *   PV_PATH_AUTO    (default) comb when keys repeat >= 16x on average in a chunk, else Straus;
- *                   decided on the device, so pv_verify_batch_device stays asynchronous. */
+ *   PV_PATH_AUTO    (default) comb when a chunk's distinct keys <= 0.021 n - 640 (from measured
+ *                   per-key and per-request costs: large batches with repeated signers), else
+ *                   Straus; decided on the device, so pv_verify_batch_device stays asynchronous. */
 #define PV_PATH_AUTO 0
 #define PV_PATH_STRAUS 1
 #define PV_PATH_COMB 2

@@ -36,7 +36,6 @@ static constexpr int PV_BLOCK = 256;
 #endif
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
-static constexpr uint32_t PV_COMB_MIN_REUSE = 16; // AUTO: comb path iff distinct keys <= requests / 16
 
 // ---------------------------------------------------------------------------------------- device
 
@@ -187,6 +186,12 @@ struct Gate {
 //   key_flag [kcap]    libsodium key checks passed (canonical, not small-order, decompresses)
 //   bases    [kcap][32][10] uint4    [256^i](-A), extended
 //   ctab     [kcap][32][129][10] uint4  T_A, cached form
+// Key-sorted processing order ("slots"): after dedup the requests of each key occupy a contiguous
+// range of slots, so consecutive lanes and waves read the same key's table rows (L2-resident)
+// instead of 1,024 keys' tables at random. Per-request kernels of the comb path run in slot order:
+//   key_count[kcap], key_cursor[kcap]   requests per key, then the next free slot of each key
+//   slot_req [stride]                   slot -> request index;  req_pos [stride] request -> slot
+//   skey     [stride]                   slot -> key id;         sverdict [stride / 64] slot verdicts
 struct KeyWork {
     uint32_t* slot;
     uint32_t* slot_id;
@@ -196,6 +201,12 @@ struct KeyWork {
     uint32_t* key_flag;
     uint4* bases;
     uint4* ctab;
+    uint32_t* key_count;
+    uint32_t* key_cursor;
+    uint32_t* slot_req;
+    uint32_t* req_pos;
+    uint32_t* skey;
+    uint64_t* sverdict;
     uint32_t hmask;
     uint32_t kcap;
     uint32_t seed;
@@ -347,6 +358,71 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, Key
         kw.slot_id[s] = id;
         kw.key_owner[id] = i;
     }
+}
+
+// Sort 1/3: dense key id per request (req_key: slot -> id) and requests per key.
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_count_kernel(uint64_t n, KeyWork kw) {
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n || *kw.nkeys > kw.kcap) return;  // over capacity: the Straus path runs, ids unused
+    const uint32_t id = kw.slot_id[kw.req_key[i]];
+    kw.req_key[i] = id;
+    atomicAdd(&kw.key_count[id], 1u);
+}
+
+// Sort 2/3: exclusive prefix sum of key_count into key_cursor (one workgroup; nkeys <= kcap).
+__global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
+    __shared__ uint32_t part[1024];
+    const uint32_t nk = *kw.nkeys;
+    if (nk > kw.kcap) return;
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nk + 1023) / 1024;
+    uint32_t sum = 0;
+    for (uint32_t j = 0; j < per; j++) {
+        const uint32_t id = t * per + j;
+        if (id < nk) sum += kw.key_count[id];
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the partials
+        const uint32_t v = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t base = t ? part[t - 1] : 0u;
+    for (uint32_t j = 0; j < per; j++) {
+        const uint32_t id = t * per + j;
+        if (id < nk) {
+            kw.key_cursor[id] = base;
+            base += kw.key_count[id];
+        }
+    }
+}
+
+// Sort 3/3: each request takes the next slot of its key (order within a key is arbitrary).
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_scatter_kernel(uint64_t n, KeyWork kw, Gate gate) {
+    if (!gate.comb()) return;
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t id = kw.req_key[i];
+    const uint32_t pos = atomicAdd(&kw.key_cursor[id], 1u);
+    kw.slot_req[pos] = i;
+    kw.req_pos[i] = pos;
+    kw.skey[pos] = id;
+}
+
+// Slot verdict bits back to request order: one ballot per 64 requests.
+__global__ __launch_bounds__(PV_BLOCK) void pv_unpermute_kernel(uint64_t n, KeyWork kw, uint64_t* __restrict__ verdict,
+                                                                 Gate gate) {
+    if (!gate.comb()) return;
+    const uint32_t r = blockIdx.x * PV_BLOCK + threadIdx.x;
+    bool ok = false;
+    if (r < n) {
+        const uint32_t s = kw.req_pos[r];
+        ok = (kw.sverdict[s >> 6] >> (s & 63)) & 1;
+    }
+    const uint64_t bits = __ballot(ok);
+    if ((threadIdx.x & 63) == 0 && r < n) verdict[r >> 6] = bits;
 }
 
 struct DevBases {
@@ -562,9 +638,10 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
                                                                     const uint8_t* __restrict__ pk, Work wk,
                                                                     KeyWork kw, Gate gate) {
     if (!gate.comb()) return;
-    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
     if (i >= n) return;
-    const uint64_t o0 = off[i], o1 = off[i + 1];
+    const uint32_t r = kw.slot_req[i];                         // request
+    const uint64_t o0 = off[r], o1 = off[r + 1];
     const uint64_t smlen = o1 - o0;
     const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
     const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
@@ -574,13 +651,12 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
         in.R[q] = mw.dw(q);
         in.S[q] = mw.dw(8 + q);
     }
-    pv_load_pk(in.A, pk, i);
+    pv_load_pk(in.A, pk, r);
     bool ok = pv_sig_ok(in, smlen);
     uint32_t k[8];
     pv_hash_k(k, in, smlen, mw);
-    // the key's own checks (key_flag) are written by pv_key_chain_kernel on the key stream, which
-    // runs concurrently with this kernel: pv_comb_msm_kernel folds them into flags[i]
-    kw.req_key[i] = kw.slot_id[kw.req_key[i]];
+    // the key's own checks (key_flag) are written by the chain kernel on the key stream, which
+    // runs concurrently with this kernel: pv_comb_a_kernel folds them into flags[slot]
     uint32_t ek[8], fs[8];
     sc_recode256(ek, k);
     sc_recode65536(fs, in.S);
@@ -619,9 +695,9 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                Gate gate) {
     if (!gate.comb()) return;
-    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
     if (i >= n) return;
-    const uint32_t id = kw.req_key[i];
+    const uint32_t id = kw.skey[i];
     const uint32_t S = (uint32_t)wk.stride;
     const Soa qs(wk.q, 40, wk.stride);
     ge_p3 acc;
@@ -676,11 +752,13 @@ struct DevEncSink {
     const uint8_t* sm;
     const uint64_t* off;
     uint64_t* verdict;
+    const uint32_t* slot_req;  // comb path: slot -> request (verdict words are then slot-ordered)
     uint32_t w, l;
     uint64_t n;
     __device__ __forceinline__ void operator()(int t, const uint32_t enc[8], bool use) const {
         const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
-        const uint32_t rr = r < n ? r : 0;
+        const uint32_t rr0 = r < n ? r : 0;
+        const uint32_t rr = slot_req ? slot_req[rr0] : rr0;
         const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[rr]);
         const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
         uint32_t R[8];
@@ -694,7 +772,9 @@ struct DevEncSink {
 };
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* __restrict__ sm,
                                                                  const uint64_t* __restrict__ off, uint64_t n,
-                                                                 Work wk, uint64_t* __restrict__ verdict) {
+                                                                 Work wk, uint64_t* __restrict__ verdict,
+                                                                 KeyWork kw, Gate gate) {
+    const bool comb = gate.comb();
     const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t w = g >> 6, l = g & 63;
     const DevEncSrc src{Soa(wk.q, 40, wk.stride), w, l, n};
@@ -704,7 +784,8 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* _
         const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
         use[t] = r < n && wk.flags[r < n ? r : 0] != 0;
     }
-    pv_encode_batch_stream(src, use, DevEncSink{sm, off, verdict, w, l, n});
+    pv_encode_batch_stream(src, use, DevEncSink{sm, off, comb ? kw.sverdict : verdict, comb ? kw.slot_req : nullptr,
+                                                w, l, n});
 }
 
 // ------------------------------------------------------------------------------------------ host
@@ -805,12 +886,18 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
         };
         int rc = mark(PV_STAGE_KEYS);
         if (rc) return rc;
-        // Path choice: the comb path pays ~one verification's work per 60 requests for each
-        // distinct key (chain + 4,128-entry table), so AUTO takes it when keys repeat >= 16x on
-        // average; the decision itself is made on the device from the dedup count (Gate).
+        // Path choice (measured round-1 costs on MI355X): the comb path pays ~0.3 ms of fixed
+        // work per chunk (dedup, sort, chain latency) and ~0.47 us per distinct key (its 4,128-entry
+        // table), then ~3 ns per request against ~13 ns on the Straus path. AUTO therefore takes it
+        // when distinct keys <= (10 ns x n - 0.3 ms) / 0.47 us ~= 0.021 n - 640; the decision is
+        // made on the device from the dedup count (Gate), so nothing synchronises.
         uint32_t limit = 0;
-        if (g_ctx.path == PV_PATH_COMB) limit = g_ctx.kw.kcap;
-        else if (g_ctx.path == PV_PATH_AUTO) limit = (uint32_t)std::min<uint64_t>(g_ctx.kw.kcap, m / PV_COMB_MIN_REUSE);
+        if (g_ctx.path == PV_PATH_COMB) {
+            limit = g_ctx.kw.kcap;
+        } else if (g_ctx.path == PV_PATH_AUTO) {
+            const int64_t l = ((int64_t)m * 21 - 640000) / 1000;
+            limit = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(g_ctx.kw.kcap, l));
+        }
         Gate gate{nullptr, 0};
         g_ctx.last_limit = limit;
         if (limit > 0) {
@@ -822,6 +909,14 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
             hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             gate = Gate{kw.nkeys, limit};
+            // key-sorted slot order for the per-request comb kernels
+            PV_HIP(hipMemsetAsync(kw.key_count, 0, (uint64_t)kw.kcap * 4, stream), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_key_count_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(1024), 0, stream, kw);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_key_scatter_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             // the per-key chain (few, long-latency lanes) and the table fill run on kstream,
             // overlapped with the per-request prep on the main stream
             PV_HIP(hipEventRecord(g_ctx.ev_keys_ready, stream), PV_ERR_LAUNCH);
@@ -870,8 +965,13 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
         if ((rc = mark(PV_STAGE_ENCODE))) return rc;
         const unsigned egrid = (unsigned)((m + PV_BLOCK * PV_ENC_BATCH - 1) / (PV_BLOCK * PV_ENC_BATCH));
         hipLaunchKernelGGL(pv_encode_kernel, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                           g_ctx.work, d_verdict + c0 / 64);
+                           g_ctx.work, d_verdict + c0 / 64, g_ctx.kw, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if (limit > 0) {
+            hipLaunchKernelGGL(pv_unpermute_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.kw,
+                               d_verdict + c0 / 64, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        }
         if ((rc = mark(PV_NSTAGES))) return rc;
     }
     return PV_OK;
@@ -933,6 +1033,12 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * 160), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_count, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_cursor, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.slot_req, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.req_pos, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.skey, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.sverdict, S / 64 * 8), PV_ERR_ALLOC);
         std::vector<uint32_t> bc((size_t)PV_BCOMB_POS * PV_BCOMB_ENT * PV_BCOMB_STRIDE);
         {
             ge_p3 base[PV_BCOMB_POS];
@@ -963,7 +1069,9 @@ void pv_shutdown(void) {
     if (g_ctx.work.q) (void)hipFree(g_ctx.work.q);
     for (void* p : {(void*)g_ctx.kw.slot, (void*)g_ctx.kw.slot_id, (void*)g_ctx.kw.req_key, (void*)g_ctx.kw.nkeys,
                     (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
-                    (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb})
+                    (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb, (void*)g_ctx.kw.key_count,
+                    (void*)g_ctx.kw.key_cursor, (void*)g_ctx.kw.slot_req, (void*)g_ctx.kw.req_pos,
+                    (void*)g_ctx.kw.skey, (void*)g_ctx.kw.sverdict})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : g_ctx.ev) (void)hipEventDestroy(e);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
