@@ -153,3 +153,25 @@ def test_smoke_entry():
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     m.smoke()
+
+
+def test_two_chunks_every_path(native, nym1m):
+    """More requests than one launch chunk (2^20): the second chunk is small, so AUTO takes the
+    Straus path there while the first chunk goes keyed-comb; forced paths cover both chunks.
+    A few corrupted records in each chunk must be rejected on every path."""
+    blob, off, pks = nym1m
+    extra = 100000
+    blob2 = np.concatenate([blob, blob[:int(off[extra])]])
+    off2 = np.concatenate([off, off[1:extra + 1] + off[-1]])
+    pks2 = np.concatenate([pks, pks[:extra]])
+    n = len(off2) - 1
+    bad = np.array([5, 777777, (1 << 20) + 3, n - 1])
+    for i in bad:
+        blob2[int(off2[i]) + 70] ^= 1  # a message byte
+    want = np.ones(n, bool)
+    want[bad] = False
+    for path in (native.PV_PATH_AUTO, native.PV_PATH_COMB, native.PV_PATH_STRAUS):
+        native.set_path(path)
+        got = native.verify_sm_batch(blob2, off2, pks2)
+        native.set_path(native.PV_PATH_AUTO)
+        assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
