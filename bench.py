@@ -111,7 +111,7 @@ def cpu_baseline(blob, off, pks, sample):
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present."""
-    p = os.path.join(ROOT, "profiles", "pmc_msm_latest.json")
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(p):
         return None
     try:

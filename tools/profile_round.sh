@@ -13,7 +13,7 @@ timeout -k 10 300 python3 tools/nym_workload.py --out $DS || exit $?
 BENCH="python3 bench.py --dataset $DS --no-cpu-baseline --no-host-path"
 echo "== kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- $BENCH > $OUT/bench_traced.json 2> $OUT/trace.log || exit $?
-PMCB="$BENCH --steps 3 --warmup 1 --no-straus"
+PMCB="$BENCH --steps 3 --warmup 1"
 i=0
 for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
