@@ -137,6 +137,77 @@ int pv_resolve_verkeys(const char* idr_chars, const uint64_t* idr_off, const cha
                        const uint64_t* vk_off, const uint8_t* has_verkey, uint64_t n, uint8_t* pk_out,
                        uint8_t* status);
 
+/* Device ingress front end: everything between the received strings and
+ * crypto_sign_open, for a whole batch, on the GPU, then the verification itself. Replaces per
+ * signature: plenum/server/client_authn.py:97 b58decode(sig), plenum/common/verifier.py:24-51
+ * DidVerifier(verkey, identifier) key resolution, stp_core/crypto/nacl_wrappers.py:108
+ * `signature + msg`. Inputs (device pointers, offsets relative to their blob):
+ *   n verifications: sig_chars/sig_off  base58 signature strings (after str.rstrip(); non-ASCII
+ *                                       bytes are invalid characters)
+ *                    msg_idx[n]         message M of verification i (signing-serialized request)
+ *                    signer_idx[n]      signer of verification i
+ *   n_msgs messages: msg/msg_off        (msg_bytes_total = sum over i of len(M[msg_idx[i]]), it
+ *                                       sizes the assembly buffer; an understatement empties
+ *                                       every record and reports status 3, never a fault)
+ *   n_signers:       idr_chars/idr_off  identifier strings ("" = None), vk_chars/vk_off verkey
+ *                                       strings as getVerkey returned them, vk_present[u] = 0 when
+ *                                       the verkey is None
+ * Outputs: verdict bit i (as pv_verify_batch: crypto_sign_open(b58decode(sig) || M, key) == 0) and
+ * status[i]:
+ *   0       verified (the verdict bit is the result)
+ *   1       the signature is not base58 (InvalidSignatureFormat)
+ *   2       the signature decodes to more than 96 bytes (not assembled; verdict 0)
+ *   3       msg_idx / signer_idx out of range, or msg_bytes_total too small (verdict 0)
+ *   16 + k  signer key resolution status k (pv_resolve_verkeys codes; k = 3: no key, verify() is
+ *           False) — the verdict bit is 0
+ * Enqueued on `stream` (NULL = the library stream); workspace is the library's, so concurrent calls
+ * must share one stream. pv_ingress_verify is the same on host buffers (synchronous; validates
+ * offsets and indices and returns PV_ERR_ARG instead of launching on bad input).
+ * pv_ingress_front_ms: device time of the most recent call's front end (decode, resolve, scan,
+ * assembly), excluding the verification kernels. */
+int pv_ingress_verify_device(const char* d_sig_chars, const uint64_t* d_sig_off, const uint32_t* d_msg_idx,
+                             const uint32_t* d_signer_idx, uint64_t n, const uint8_t* d_msg, const uint64_t* d_msg_off,
+                             uint64_t n_msgs, uint64_t msg_bytes_total, const char* d_idr_chars,
+                             const uint64_t* d_idr_off, const char* d_vk_chars, const uint64_t* d_vk_off,
+                             const uint8_t* d_vk_present, uint64_t n_signers, uint8_t* d_status,
+                             uint64_t* d_verdict_words, void* stream);
+int pv_ingress_verify(const char* sig_chars, const uint64_t* sig_off, const uint32_t* msg_idx,
+                      const uint32_t* signer_idx, uint64_t n, const uint8_t* msg, const uint64_t* msg_off,
+                      uint64_t n_msgs, const char* idr_chars, const uint64_t* idr_off, const char* vk_chars,
+                      const uint64_t* vk_off, const uint8_t* vk_present, uint64_t n_signers, uint8_t* status,
+                      uint8_t* verdict_bits);
+int pv_ingress_front_ms(double* ms);
+
+/* Signing serialization of received JSON requests on the host, many threads:
+ * request i is the JSON text json[off[i] : off[i+1]] that ZStack.deserializeMsg decodes
+ * (stp_zmq/zstack.py:881-885); the output is the signing-serialized message
+ * (common/serializers/signing_serializer.py:35-92, serialization.py:27-36) of
+ *   PV_SER_DICT     json.loads(text)
+ *   PV_SER_AUTHN    json.loads(text) minus top-level {signature, signatures, fees}
+ *                   (CoreAuthMixin.authenticate, plenum/server/client_authn.py:198,232)
+ *   PV_SER_REQUEST  Request(**json.loads(text)).as_dict minus those keys (Node.verifySignature,
+ *                   plenum/server/node.py:2636-2650), and digest[32 i .. 32 i + 32) =
+ *                   sha256(serialize(signingState())) (plenum/common/request.py:86-121)
+ * written to msg_out[msg_off[i] : msg_off[i+1]]. plugin_fields: NUL-separated names ending with an
+ * empty name (PLUGIN_CLIENT_REQUEST_FIELDS, request.py:37-39), or NULL. status[i]:
+ *   PV_SER_OK          serialized
+ *   PV_SER_INVALID     json.loads would raise (bad UTF-8, bad JSON, control characters...)
+ *   PV_SER_NOT_OBJECT  the document is not a JSON object
+ *   PV_SER_DEFER       valid, but outside what is reproduced bit-for-bit here (floats, NaN/Infinity,
+ *                      lone surrogates, nesting > 512, ints > 4,300 digits, a request-mode digest
+ *                      whose Python evaluation raises): the caller serializes it in Python
+ * Returns PV_ERR_ARG with msg_off[n] = the bytes needed when msg_cap is too small. */
+#define PV_SER_DICT 0
+#define PV_SER_AUTHN 1
+#define PV_SER_REQUEST 2
+#define PV_SER_OK 0
+#define PV_SER_INVALID 1
+#define PV_SER_NOT_OBJECT 2
+#define PV_SER_DEFER 3
+int pv_signing_serialize_json(const char* json, const uint64_t* off, uint64_t n, int mode, const char* plugin_fields,
+                              int threads, uint8_t* msg_out, uint64_t msg_cap, uint64_t* msg_off, uint8_t* digest,
+                              uint8_t* status);
+
 /* Multi-GPU: one process per GPU. pv_comm_unique_id on rank 0, broadcast the 128 bytes by any
  * channel, pv_comm_init on every rank (after pv_init). pv_allgather_verdicts gathers
  * words_per_rank 64-bit verdict words from every rank into d_all (nranks * words_per_rank) with

@@ -22,6 +22,7 @@
 #include "btable.h"
 #include "comb.h"
 #include "verify_core.h"
+#include "pv_internal.h"
 #include "../../include/plenum_verify.h"
 
 static constexpr int PV_BLOCK = 256;
@@ -978,6 +979,9 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
 }
 
 }  // namespace
+
+hipStream_t pv_engine_stream() { return g_ctx.stream; }
+int pv_fail(int code, const std::string& msg) { return fail(code, msg); }
 
 extern "C" {
 

@@ -1,0 +1,14 @@
+// Internal (non-ABI) hooks shared between the engine translation units of libplenum_verify.so.
+#ifndef PV_INTERNAL_H
+#define PV_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+// The library's main stream (valid after pv_init).
+hipStream_t pv_engine_stream();
+// Records `msg` as the calling thread's pv_last_error() and returns `code`.
+int pv_fail(int code, const std::string& msg);
+
+#endif  // PV_INTERNAL_H

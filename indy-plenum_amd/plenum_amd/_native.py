@@ -45,6 +45,16 @@ SIGNATURES = {
     "pv_b58encode": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]),
     "pv_resolve_verkeys": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "pv_ingress_verify_device": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
+                                 + [ctypes.c_void_p] * 5 + [ctypes.c_uint64] + [ctypes.c_void_p] * 3),
+    "pv_ingress_verify": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint64] + [ctypes.c_void_p] * 5 + [ctypes.c_uint64]
+                          + [ctypes.c_void_p] * 2),
+    "pv_signing_serialize_json": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                                 ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "pv_ingress_front_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double)]),
     "pv_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_comm_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "pv_allgather_verdicts": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
@@ -150,3 +160,48 @@ def last_path():
     p, u = ctypes.c_int(), ctypes.c_uint32()
     check(lib().pv_last_path(ctypes.byref(p), ctypes.byref(u)), "pv_last_path")
     return p.value, u.value
+
+
+def _blob(items):
+    """Concatenate byte strings -> (uint8 blob (never empty), uint64 offsets)."""
+    off = np.zeros(len(items) + 1, dtype=np.uint64)
+    if items:
+        np.cumsum(np.fromiter((len(x) for x in items), dtype=np.uint64, count=len(items)), out=off[1:])
+    joined = b"".join(items)
+    return (np.frombuffer(joined, dtype=np.uint8) if joined else np.zeros(1, np.uint8)), off
+
+
+def ingress_verify_arrays(sig_blob, sig_off, msg_blob, msg_off, msg_idx, signer_idx, idr_blob, idr_off, vk_blob,
+                          vk_off, vk_present):
+    """pv_ingress_verify on packed arrays (uint8 blobs, uint64 offsets, uint32 indices, uint8 flags):
+    GPU base58 decode of every signature, GPU key resolution per signer, device-side sm assembly
+    and verification. Returns (status uint8[n], verdict bool[n]); status codes in
+    include/plenum_verify.h."""
+    ensure_device()
+    n = len(sig_off) - 1
+    if n <= 0:
+        return np.zeros(0, np.uint8), np.zeros(0, bool)
+    status = np.zeros(n, np.uint8)
+    bits = np.zeros((n + 7) // 8, np.uint8)
+    c = np.ascontiguousarray
+    args = [c(sig_blob, np.uint8), c(sig_off, np.uint64), c(msg_idx, np.uint32), c(signer_idx, np.uint32),
+            c(msg_blob, np.uint8), c(msg_off, np.uint64), c(idr_blob, np.uint8), c(idr_off, np.uint64),
+            c(vk_blob, np.uint8), c(vk_off, np.uint64), c(vk_present, np.uint8)]
+    sb, so, mi, si, mb, mo, ib, io, vb, vo, vp = [a if a.size else np.zeros(1, a.dtype) for a in args]
+    check(lib().pv_ingress_verify(_ptr(sb), _ptr(so), _ptr(mi), _ptr(si), n, _ptr(mb), _ptr(mo), len(msg_off) - 1,
+                                  _ptr(ib), _ptr(io), _ptr(vb), _ptr(vo), _ptr(vp), len(idr_off) - 1,
+                                  _ptr(status), _ptr(bits)), "pv_ingress_verify")
+    return status, np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+
+
+def ingress_verify(sigs, msgs, msg_idx, signer_idx, idrs, vks):
+    """ingress_verify_arrays on Python lists: sigs (n byte strings), msgs (byte strings),
+    msg_idx / signer_idx (n ints), idrs (identifier bytes per signer, b"" = None), vks (verkey
+    bytes or None per signer)."""
+    sig_b, sig_o = _blob(list(sigs))
+    msg_b, msg_o = _blob(list(msgs))
+    idr_b, idr_o = _blob(list(idrs))
+    vk_b, vk_o = _blob([v if v is not None else b"" for v in vks])
+    vkp = np.array([v is not None for v in vks], dtype=np.uint8)
+    return ingress_verify_arrays(sig_b, sig_o, msg_b, msg_o, np.asarray(msg_idx, np.uint32),
+                                 np.asarray(signer_idx, np.uint32), idr_b, idr_o, vk_b, vk_o, vkp)
