@@ -10,6 +10,9 @@ and stubs for zmq/jsonpickle that the hot path never calls. Outputs (all JSON, d
   authn.json         CoreAuthNr.authenticate / authenticate_multi outcomes on signed requests
   reqauth.json       ReqAuthenticator.authenticate sequences (cache, query, NoAuthenticatorFound)
   verdicts.json      libsodium crypto_sign_open verdicts on normal + adversarial (sm, pk) vectors
+  request.json       Request(**json.loads(text)): signing bytes of as_dict minus the excluded keys,
+                     digest, payload_digest (the wire path's C++ serializer and Request mirror)
+Run all generators, or name some: python tests/golden/make_golden.py request.json
 """
 import json
 import os
@@ -285,9 +288,63 @@ def gen_verdicts():
     return out
 
 
+# ----------------------------------------------------------------------------- Request (wire path)
+def request_texts():
+    """JSON texts of client requests in the shapes the ingress sees (generated here, data only)."""
+    did, did2 = "V4SGRU86Z58d6TV7PBUe6f", "CzkavE58zgX7rUMrzSinLr"
+    nym = {"type": "1", "dest": did2, "verkey": "~CoRER63DVYnWZtK8uAzNbx", "alias": "u00000001"}
+    taa = {"taaDigest": "ab" * 32, "mechanism": "service_agreement", "time": 1700000000}
+    docs = [
+        {"identifier": did, "reqId": 1700000000000001, "protocolVersion": 2, "operation": nym,
+         "taaAcceptance": taa, "signature": "3v5Xk"},
+        {"identifier": did, "reqId": 1, "operation": nym, "signatures": {did: "s1", did2: "s2"}},
+        {"reqId": 2, "operation": nym, "signatures": {did2: "s2", did: "s1"}},
+        {"identifier": "", "reqId": 3, "operation": nym, "signatures": {did2: "a", "Abc": "b"}},
+        {"identifier": None, "reqId": 4, "operation": nym, "signature": "x"},
+        {"identifier": did, "reqId": 5, "operation": nym, "signature": "x", "endorser": did2, "fees": [1, 2],
+         "unknownField": {"z": 1}, "protocolVersion": None, "taaAcceptance": None},
+        {"identifier": did, "reqId": 6, "operation": {"type": "101", "data": {"nested": [1, None, True, False],
+                                                                            "u": "\u00fcn\u00efc\u00f6d\u00e9 \u20ac"}},
+         "signature": "x"},
+        {"identifier": did, "reqId": -0, "operation": {"type": "1", "k": [[], {}, [[1]], {"a": {"b": {}}}]},
+         "signature": "x"},
+        {"identifier": 0, "reqId": None, "operation": None, "signatures": {}},
+        {"identifier": did, "reqId": 7, "operation": nym, "signature": None, "signatures": None},
+        {"identifier": did, "reqId": 10 ** 30, "operation": {"type": "1", "big": -10 ** 25}, "signature": "x"},
+        {"identifier": did, "reqId": 8, "operation": {"type": "1", "esc": "tab\t nl\n quote\" bs\\ slash/"},
+         "signature": "x"},
+        {"identifier": did, "reqId": 9, "operation": {"type": "1", "astral": "\ud83d\ude00"}, "signature": "x"},
+    ]
+    texts = [json.dumps(d) for d in docs]
+    texts += [
+        '{"identifier": "%s", "reqId": 11, "operation": {"type": "1", "a": 1, "a": 2}, "signature": "x"}' % did,
+        '{"reqId": 12, "reqId": 13, "operation": {"type": "1"}, "identifier": "%s", "signature": "y"}' % did,
+        '{ "identifier" : "%s" ,\n "reqId":14,"operation":{"type":"1","escaped\\u0041key":"\\u0041"},'
+        '"signature":"z" }' % did,
+        '{"identifier": "%s", "reqId": 15, "operation": {"type": "1", "e": "\\u00e9", "raw": "é中"},'
+        ' "signature": "x"}' % did,
+        '{"identifier": "%s", "reqId": -0, "operation": {"type": "1", "neg": -12, "zero": 0}}' % did,
+    ]
+    return texts
+
+
+def gen_request():
+    out = []
+    excluded = {"signature", "signatures", "fees"}
+    for text in request_texts():
+        def run():
+            req = Request(**json.loads(text))
+            view = {k: v for k, v in req.as_dict.items() if k not in excluded}
+            return {"signing": serialize_msg_for_signing(view).hex(), "digest": req.digest,
+                    "payload_digest": req.payload_digest}
+        out.append({"text": text, "out": outcome(run)})
+    return out
+
+
+GENERATORS = {"serializer.json": lambda: gen_serializer(), "didverifier.json": lambda: gen_didverifier(),
+              "authn.json": lambda: gen_authn(), "reqauth.json": lambda: gen_reqauth(),
+              "verdicts.json": lambda: gen_verdicts(), "request.json": lambda: gen_request()}
+
 if __name__ == "__main__":
-    dump("serializer.json", gen_serializer())
-    dump("didverifier.json", gen_didverifier())
-    dump("authn.json", gen_authn())
-    dump("reqauth.json", gen_reqauth())
-    dump("verdicts.json", gen_verdicts())
+    for name in sys.argv[1:] or list(GENERATORS):
+        dump(name, GENERATORS[name]())
