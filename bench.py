@@ -114,6 +114,95 @@ def cpu_baseline(blob, off, pks, sample, target_s=10.0):
             "accepted": int(acc), "seconds": round(dt, 3)}
 
 
+def ingress_leg(n, blob, off, wire, steps, warmup):
+    """what happens before pv_verify_batch_device, measured on the same workload.
+      host   C++ signing serialization + Request.digest of every received JSON request
+             (pv_signing_serialize_json, 16 threads) — the host-serialization overhead
+      device pv_ingress_verify_device: GPU base58 decode of every signature, key resolution for
+             the 1,024 signers, sm assembly, verification (inputs resident in HBM)
+      e2e    authenticate_wire_batch (JSON bytes -> identifier sets, Python glue included) on 64k
+    Returns the bench-line object."""
+    from plenum_amd.client_authn import CoreAuthNr
+    from plenum_amd.req_authenticator import ReqAuthenticator
+    from plenum_amd.wire import PV_SER_REQUEST, authenticate_wire_batch, signing_serialize_packed
+    L = _native.lib()
+    wblob, woff, sblob, soff = wire
+    threads = min(16, len(os.sched_getaffinity(0)))
+    signing_serialize_packed(wblob[:int(woff[1024])], woff[:1025], PV_SER_REQUEST, threads)
+    t0 = time.perf_counter()
+    st, mblob, moff, _ = signing_serialize_packed(wblob, woff, PV_SER_REQUEST, threads)
+    ser_s = time.perf_counter() - t0
+    # the serializer's messages must be the ones the requests were signed over
+    starts = off[:-1] + 64
+    same = bool((st == 0).all()) and np.array_equal(np.diff(moff), off[1:] - starts)
+    if same:
+        idx = np.arange(0, n, 4099)
+        same = all(mblob[int(moff[i]):int(moff[i + 1])].tobytes() == blob[int(starts[i]):int(off[i + 1])].tobytes()
+                   for i in idx)
+    pool = nym_workload._pool()
+    idrs = [p["did"].encode() for p in pool]
+    vks = [p["abbr"].encode() for p in pool]
+    ib, io = _native._blob(idrs)
+    vb, vo = _native._blob(vks)
+    vp = np.ones(len(pool), np.uint8)
+    msg_idx = np.arange(n, dtype=np.uint32)
+    signer_idx = (np.arange(n, dtype=np.uint64) % len(pool)).astype(np.uint32)
+    db = DeviceBatch(np.zeros(1, np.uint8), np.zeros(2, np.uint64), np.zeros((1, 32), np.uint8))
+    d = {k: db._put(a, a.nbytes) for k, a in (("s", sblob), ("so", soff), ("m", mblob[:int(moff[-1]) + 8]),
+                                                ("mo", moff), ("mi", msg_idx), ("si", signer_idx), ("i", ib),
+                                                ("io", io), ("v", vb), ("vo", vo), ("vp", vp))}
+    d_status = db._alloc(n)
+    d_ver = db._alloc((n + 63) // 64 * 8)
+    mtotal = int(moff[-1])
+
+    def step():
+        _native.check(L.pv_ingress_verify_device(d["s"], d["so"], d["mi"], d["si"], n, d["m"], d["mo"], n, mtotal,
+                                                 d["i"], d["io"], d["v"], d["vo"], d["vp"], len(pool), d_status,
+                                                 d_ver, None), "pv_ingress_verify_device")
+
+    for _ in range(warmup):
+        step()
+    _native.check(L.pv_sync(), "pv_sync")
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    _native.check(L.pv_sync(), "pv_sync")
+    dev_s = (time.perf_counter() - t0) / steps
+    front = ctypes.c_double()
+    _native.check(L.pv_ingress_front_ms(ctypes.byref(front)), "pv_ingress_front_ms")
+    status = np.zeros(n, np.uint8)
+    _native.check(L.pv_memcpy_d2h(status.ctypes.data, d_status, n), "pv_memcpy_d2h")
+    ver = np.unpackbits(db.verdict_words(d_ver, (n + 63) // 64).view(np.uint8), bitorder="little")[:n]
+    db.free()
+    # end to end through the Python surface on a 64k sample
+    k = min(n, 1 << 16)
+    core = CoreAuthNr(["1"], ["105"], [], state=None)
+    for p in pool:
+        core.addIdr(p["did"], p["abbr"])
+    ra = ReqAuthenticator()
+    ra.register_authenticator(core)
+    raws = [wblob[int(woff[i]):int(woff[i + 1])].tobytes() for i in range(k)]
+    tm = {}
+    t0 = time.perf_counter()
+    res = authenticate_wire_batch(ra, raws, threads=threads, timings=tm)
+    e2e_s = time.perf_counter() - t0
+    e2e_ok = all(r == {pool[i % len(pool)]["did"]} for i, (_, r) in enumerate(res))
+    return {
+        "host_signing_serialize": {"requests": n, "threads": threads, "seconds": round(ser_s, 4),
+                                   "requests_per_s": round(n / ser_s, 1),
+                                   "us_per_request_per_thread": round(ser_s * threads * 1e6 / n, 3),
+                                   "messages_match_signed": bool(same)},
+        "device_ingress": {"verifies_per_s": round(n / dev_s, 1), "ms_per_step": round(dev_s * 1e3, 3),
+                           "front_end_ms": round(front.value, 4),
+                           "note": "GPU b58 decode + key resolution + sm assembly + verification, HBM-resident",
+                           "verdicts_ok": bool((status == 0).all() and ver.all())},
+        "wire_batch_e2e": {"requests": k, "requests_per_s": round(k / e2e_s, 1),
+                           "stages_s": {x: round(tm[x], 4) for x in ("serialize_s", "plan_s", "gpu_s", "finish_s")},
+                           "ok": bool(e2e_ok), "note": "JSON bytes -> identifier sets incl. json.loads, getVerkey "
+                                                      "and the cache in Python (one host thread)"},
+    }
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
@@ -139,6 +228,7 @@ def main():
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-straus", action="store_true", help="skip the secondary Straus-path measurement")
     ap.add_argument("--dataset", default=None, help="npz from tools/nym_workload.py (profiling runs: no fork)")
+    ap.add_argument("--no-ingress", action="store_true", help="skip the ingress / host-serialization measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -155,9 +245,12 @@ def main():
         dist = tdist
 
     t0 = time.perf_counter()
+    wire = None
     if args.dataset and os.path.exists(args.dataset):
         blob, off, pks, lo = nym_workload.load(args.dataset)
         assert lo == rank * n and len(off) - 1 == n, "dataset does not match this rank's shard"
+    elif world == 1 and not args.no_ingress:
+        blob, off, pks, *wire = nym_workload.generate_wire(rank * n, n)
     else:
         blob, off, pks = nym_workload.generate(rank * n, n)
     gen_s = time.perf_counter() - t0
@@ -289,6 +382,8 @@ def main():
         result["host_path"] = {"verifies_per_s": round(hsamp / dt, 1), "requests": hsamp, "ok": bool(v.all())}
         result["host_prep"] = {"workload_generation_s": round(gen_s, 2), "note": "serialize + sign, %d workers" % min(
             16, os.cpu_count() or 1)}
+    if rank == 0 and world == 1 and wire:
+        result["ingress"] = ingress_leg(n, blob, off, wire, max(3, args.steps // 4), 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(blob, off, pks, min(args.cpu_sample, n), args.cpu_seconds)
         result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)

@@ -132,9 +132,16 @@ def signing_bytes(req: Request) -> bytes:
 def signing_serialize_json(raws, mode=PV_SER_REQUEST, threads=16, plugin_fields=None):
     """pv_signing_serialize_json over JSON texts (bytes). Returns (status uint8[n], message blob
     uint8, offsets uint64[n+1], digests uint8[n, 32]) — message i is blob[off[i]:off[i+1]]."""
-    L = _native.lib()
-    n = len(raws)
     blob, off = _native._blob([r if isinstance(r, (bytes, bytearray)) else r.encode() for r in raws])
+    return signing_serialize_packed(blob, off, mode, threads, plugin_fields)
+
+
+def signing_serialize_packed(blob, off, mode=PV_SER_REQUEST, threads=16, plugin_fields=None):
+    """signing_serialize_json on texts already packed as (uint8 blob, uint64 offsets[n+1])."""
+    L = _native.lib()
+    n = len(off) - 1
+    blob = np.ascontiguousarray(blob, np.uint8) if len(blob) else np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
     names = PLUGIN_CLIENT_REQUEST_FIELDS if plugin_fields is None else plugin_fields
     pf = b"".join(x.encode() + b"\0" for x in names) + b"\0"
     status = np.zeros(max(n, 1), np.uint8)

@@ -84,26 +84,54 @@ def _pool():
     return _POOL_CACHE
 
 
+def wire_text(i, s, sig_b58):
+    """The request as a client sends it: json.dumps(request_dict(i, s) + signature), rendered
+    directly (checked against json.dumps on a sample)."""
+    h = hashlib.sha256(struct.pack("<Q", i)).digest()
+    return ('{"identifier": "%s", "reqId": %d, "protocolVersion": 2, "operation": {"type": "1", "dest": "%s", '
+            '"verkey": "~%s", "alias": "u%08d"}, "taaAcceptance": {"taaDigest": "%s", "mechanism": '
+            '"service_agreement", "time": 1700000000}, "signature": "%s"}'
+            % (s["did"], 1700000000000000 + i, b58(h[:16]), b58(h[16:]), i, TAA_DIGEST, sig_b58)).encode()
+
+
 def _sign_range(args):
-    lo, hi = args
+    lo, hi, wire = args
     pool = _pool()
     lib = sodium()
     sig = ctypes.create_string_buffer(64)
-    out_sm, out_pk = [], []
+    out_sm, out_pk, out_wire, out_sig = [], [], [], []
     for i in range(lo, hi):
         s = pool[i % POOL]
         m = message(i, s)
         lib.crypto_sign_detached(sig, None, m, ctypes.c_ulonglong(len(m)), s["sk"])
         out_sm.append(sig.raw + m)
         out_pk.append(s["vk"])
-    return b"".join(out_sm), [len(x) for x in out_sm], b"".join(out_pk)
+        if wire:
+            sb = b58(sig.raw)
+            out_sig.append(sb.encode())
+            out_wire.append(wire_text(i, s, sb))
+    extra = ((b"".join(out_wire), [len(x) for x in out_wire], b"".join(out_sig), [len(x) for x in out_sig])
+             if wire else None)
+    return b"".join(out_sm), [len(x) for x in out_sm], b"".join(out_pk), extra
 
 
-def generate(lo, n, workers=None):
+def _offsets(lens):
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    np.cumsum(np.asarray(lens, dtype=np.uint64), out=off[1:])
+    return off
+
+
+def generate_wire(lo, n, workers=None):
+    """As generate(), plus what arrives on the wire: (blob, off, pks, wire blob, wire offsets,
+    b58 signature blob, signature offsets)."""
+    return generate(lo, n, workers, wire=True)
+
+
+def generate(lo, n, workers=None, wire=False):
     """Requests [lo, lo + n): (blob uint8, offsets uint64[n+1], pks uint8[n, 32])."""
     workers = workers or min(16, max(1, (os.cpu_count() or 1)))
     chunk = max(1, (n + workers * 4 - 1) // (workers * 4))
-    ranges = [(a, min(a + chunk, lo + n)) for a in range(lo, lo + n, chunk)]
+    ranges = [(a, min(a + chunk, lo + n), wire) for a in range(lo, lo + n, chunk)]
     if workers > 1 and n > 20000:
         ctx = mp.get_context("fork")
         with ctx.Pool(workers) as p:
@@ -115,7 +143,13 @@ def generate(lo, n, workers=None):
     off = np.zeros(n + 1, dtype=np.uint64)
     np.cumsum(lens, out=off[1:])
     pks = np.frombuffer(b"".join(p[2] for p in parts), dtype=np.uint8).reshape(n, 32)
-    return blob, off, pks
+    if not wire:
+        return blob, off, pks
+    wblob = np.frombuffer(b"".join(p[3][0] for p in parts), dtype=np.uint8)
+    woff = _offsets([x for p in parts for x in p[3][1]])
+    sblob = np.frombuffer(b"".join(p[3][2] for p in parts), dtype=np.uint8)
+    soff = _offsets([x for p in parts for x in p[3][3]])
+    return blob, off, pks, wblob, woff, sblob, soff
 
 
 def save(path, lo, n, workers=None):
