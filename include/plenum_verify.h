@@ -146,7 +146,8 @@ int pv_resolve_verkeys(const char* idr_chars, const uint64_t* idr_off, const cha
  *                                       bytes are invalid characters)
  *                    msg_idx[n]         message M of verification i (signing-serialized request)
  *                    signer_idx[n]      signer of verification i
- *   n_msgs messages: msg/msg_off        (msg_bytes_total = sum over i of len(M[msg_idx[i]]), it
+ *   n_msgs messages: msg/msg_off        (readable for 8 bytes past msg_off[n_msgs];
+ *                                       msg_bytes_total = sum over i of len(M[msg_idx[i]]), it
  *                                       sizes the assembly buffer; an understatement empties
  *                                       every record and reports status 3, never a fault)
  *   n_signers:       idr_chars/idr_off  identifier strings ("" = None), vk_chars/vk_off verkey

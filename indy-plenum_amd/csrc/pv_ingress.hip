@@ -65,10 +65,17 @@ struct B58Dec {
     __device__ __forceinline__ uint32_t len() const { return zeros + nbytes; }
 };
 
-__device__ void pv_b58_decode(const uint8_t* __restrict__ s, uint64_t len, B58Dec& o) {
-    while (len > 0 && pv_ascii_ws(s[len - 1])) len--;
+// Character sources for the decoder: global memory, or a workgroup's span staged in LDS.
+struct GlobalChars {
+    const uint8_t* p;
+    __device__ __forceinline__ uint32_t operator()(uint64_t i) const { return p[i]; }
+};
+
+template <class Src>
+__device__ void pv_b58_decode(const Src& s, uint64_t len, B58Dec& o) {
+    while (len > 0 && pv_ascii_ws(s(len - 1))) len--;
     uint64_t z = 0;
-    while (z < len && s[z] == '1') z++;
+    while (z < len && s(z) == '1') z++;
 #pragma unroll
     for (int l = 0; l < PV_B58_LIMBS; l++) o.limb[l] = 0;
     bool bad = false, ovf = false;
@@ -76,7 +83,7 @@ __device__ void pv_b58_decode(const uint8_t* __restrict__ s, uint64_t len, B58De
         const uint32_t g = (uint32_t)umin64(5, len - i);
         uint32_t mul = 1, add = 0;
         for (uint32_t k = 0; k < g; k++) {
-            const int d = pv_b58_digit(s[i + k]);
+            const int d = pv_b58_digit(s(i + k));
             bad |= d < 0;
             add = add * 58u + (uint32_t)(d & 63);
             mul *= 58u;
@@ -97,6 +104,10 @@ __device__ void pv_b58_decode(const uint8_t* __restrict__ s, uint64_t len, B58De
     o.zeros = (uint32_t)umin64(z, 0xFFFFu);
     o.nbytes = nb;
     o.status = bad ? 1u : ((ovf || z + nb > 4u * PV_B58_LIMBS) ? 2u : 0u);
+}
+
+__device__ __forceinline__ void pv_b58_decode(const uint8_t* s, uint64_t len, B58Dec& o) {
+    pv_b58_decode(GlobalChars{s}, len, o);
 }
 
 __device__ __forceinline__ int pv_hexval(uint32_t c) {
@@ -232,13 +243,38 @@ __global__ __launch_bounds__(ING_BLOCK) void pv_ing_signer_kernel(
 //   status: 0 verified, 1 signature not base58, 2 signature decodes to > 96 bytes (not assembled),
 //           3 index out of range, 16 + k signer status k != 0 (k = 3: no key, verify() is False)
 //   siginfo: zeros | nbytes << 16 of the decoded signature; rec_len: 0 unless status == 0
+constexpr uint32_t SIG_SPAN_WORDS = 8192;  // 32 KB of LDS: the signature strings of one workgroup
+
+struct LdsChars {
+    const uint8_t* lds;
+    __device__ __forceinline__ uint32_t operator()(uint64_t i) const { return lds[i]; }
+};
+
 __global__ __launch_bounds__(ING_BLOCK) void pv_ing_sig_kernel(
     const uint8_t* __restrict__ sig_chars, const uint64_t* __restrict__ sig_off,
     const uint32_t* __restrict__ msg_idx, const uint32_t* __restrict__ signer_idx, uint64_t n,
     const uint64_t* __restrict__ msg_off, uint64_t nmsg, const uint4* __restrict__ kpk,
     const uint8_t* __restrict__ kstatus, uint64_t nsig, uint4* __restrict__ sigfix, uint4* __restrict__ pk_out,
     uint32_t* __restrict__ siginfo, uint64_t* __restrict__ rec_len, uint8_t* __restrict__ status) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // The workgroup's strings are contiguous: stage them in LDS with coalesced dword loads (each
+    // lane then parses its string from LDS instead of 88 scattered byte loads from HBM).
+    __shared__ uint32_t span[SIG_SPAN_WORDS];
+    const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x;
+    const uint64_t b1 = umin64(n, b0 + blockDim.x);
+    const uintptr_t first = (uintptr_t)(sig_chars + sig_off[b0]);
+    const uintptr_t lo = first & ~(uintptr_t)3;  // inside the allocation (allocations are 256-B aligned)
+    const uintptr_t hi = (uintptr_t)(sig_chars + sig_off[b1]);
+    const bool staged = hi - lo <= 4ull * SIG_SPAN_WORDS;
+    if (staged) {
+        const uint64_t full = (hi - lo) / 4;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(lo);
+        for (uint64_t w = threadIdx.x; w < full; w += blockDim.x) span[w] = src[w];
+        uint8_t* sb = reinterpret_cast<uint8_t*>(span);
+        for (uint64_t b = 4 * full + threadIdx.x; b < hi - lo; b += blockDim.x)
+            sb[b] = reinterpret_cast<const uint8_t*>(lo)[b];
+    }
+    __syncthreads();
+    const uint64_t i = b0 + threadIdx.x;
     if (i >= n) return;
     const uint32_t mi = msg_idx[i], si = signer_idx[i];
     uint32_t st = 0;
@@ -248,7 +284,12 @@ __global__ __launch_bounds__(ING_BLOCK) void pv_ing_sig_kernel(
         st = 3;
     } else {
         B58Dec d;
-        pv_b58_decode(sig_chars + sig_off[i], sig_off[i + 1] - sig_off[i], d);
+        const uint64_t sl = sig_off[i + 1] - sig_off[i];
+        if (staged)
+            pv_b58_decode(LdsChars{reinterpret_cast<const uint8_t*>(span) +
+                                   ((uintptr_t)(sig_chars + sig_off[i]) - lo)}, sl, d);
+        else
+            pv_b58_decode(sig_chars + sig_off[i], sl, d);
         if (d.status) {
             st = d.status;
         } else {
@@ -356,8 +397,11 @@ __global__ __launch_bounds__(SCAN_TOP) void pv_ing_scan_top_kernel(uint64_t* __r
     }
 }
 
-// 16 lanes per record: final offset, then sm = b58decode(sig) || M byte by byte (coalesced across
-// the record's lanes). On an overrun every record is emptied (verdict 0, status 3).
+// 16 lanes per record: final offset, then sm = b58decode(sig) || M. Destination dwords that lie
+// wholly inside the record are written as dwords (the message part read as an unaligned 4-byte
+// window: two aligned loads + v_alignbyte_b32); the first and last dword of a record are shared
+// with its neighbours and written byte by byte. On an overrun every record is emptied (verdict 0,
+// status 3).
 __global__ __launch_bounds__(ING_BLOCK) void pv_ing_assemble_kernel(
     uint64_t n, const uint64_t* __restrict__ local, const uint64_t* __restrict__ tile_excl,
     const uint64_t* __restrict__ rec_len, const uint32_t* __restrict__ siginfo, const uint8_t* __restrict__ sigfix,
@@ -383,8 +427,28 @@ __global__ __launch_bounds__(ING_BLOCK) void pv_ing_assemble_kernel(
     const uint32_t z = info & 0xFFFFu, nb = info >> 16, sl = z + nb;
     const uint8_t* F = sigfix + 96 * i + (96 - nb) - z;  // F[p] for z <= p < sl
     const uint8_t* M = msg + msg_off[msg_idx[i]] - sl;  // M[p] for p >= sl
-    uint8_t* dst = blob + o;
-    for (uint64_t p = sub; p < L; p += ASM_LANES) dst[p] = p < z ? 0 : (p < sl ? F[p] : M[p]);
+    auto byte_at = [&](int64_t p) -> uint32_t { return p < (int64_t)z ? 0u : (p < (int64_t)sl ? F[p] : M[p]); };
+    uint32_t* dst32 = reinterpret_cast<uint32_t*>(blob);
+    const uint64_t d0 = o >> 2, d1 = (o + L + 3) >> 2;
+    for (uint64_t D = d0 + sub; D < d1; D += ASM_LANES) {
+        const int64_t p0 = (int64_t)(4 * D) - (int64_t)o;  // record position of the dword's first byte
+        if (p0 >= 0 && p0 + 4 <= (int64_t)L) {
+            uint32_t w;
+            if (p0 >= (int64_t)sl) {
+                const uintptr_t a = (uintptr_t)(M + p0);
+                const uint32_t* ap = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+                w = __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)(a & 3));
+            } else {
+                w = byte_at(p0) | byte_at(p0 + 1) << 8 | byte_at(p0 + 2) << 16 | byte_at(p0 + 3) << 24;
+            }
+            dst32[D] = w;
+        } else {
+            for (int b = 0; b < 4; b++) {
+                const int64_t p = p0 + b;
+                if (p >= 0 && p < (int64_t)L) blob[4 * D + b] = (uint8_t)byte_at(p);
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------ host

@@ -25,7 +25,7 @@ GATED_NS = 20000
 
 
 def short(name):
-    return name.split("(")[0]
+    return name.replace("(anonymous namespace)::", "").split("(")[0]
 
 
 def kernel_stats(db):
