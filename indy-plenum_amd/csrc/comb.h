@@ -88,6 +88,15 @@ PV_HD void pv_comb_fill_block(const Table& tab, const ge_p3& P, int b) {
 }
 
 // ---------------------------------------------------------------- per-request accumulation
+// (Y+X, Y-X) of a table entry's first 20 words for a digit of sign `neg` (negation swaps them)
+PV_HD void pv_sel_pm(fe& ypx, fe& ymx, const uint32_t w[20], bool neg) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        ypx.v[i] = neg ? w[10 + i] : w[i];
+        ymx.v[i] = neg ? w[i] : w[10 + i];
+    }
+}
+
 // acc + sign(e) T[|e|] for a cached-form table entry (pv_add_a's arithmetic, entry via `load`).
 template <class Entry>
 PV_HD void pv_comb_add_cached(ge_p1p1& r, const ge_p3& p, const Entry& ent, int e) {
@@ -96,11 +105,7 @@ PV_HD void pv_comb_add_cached(ge_p1p1& r, const ge_p3& p, const Entry& ent, int 
     fe ypx, ymx, t, a, b, c, d;
     uint32_t w[20];
     ent.load_half(j, 0, w);
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-        ypx.v[i] = neg ? w[10 + i] : w[i];
-        ymx.v[i] = neg ? w[i] : w[10 + i];
-    }
+    pv_sel_pm(ypx, ymx, w, neg);
     fe_sub(t, p.Y, p.X);
     fe_mul(a, t, ymx);
     fe_add(t, p.Y, p.X);
@@ -128,6 +133,111 @@ PV_HD void pv_comb_add_cached(ge_p1p1& r, const ge_p3& p, const Entry& ent, int 
 // arows.row(i) / brows.row(j) give the A row of radix-256 position i and the B row of radix-65536
 // position j (objects with load_half / load_part); dig holds the packed digits (ek: 4 signed bytes
 // of k per word, fs: 2 signed halfwords of S per word).
+
+// Software-pipelined variant (PV_COMB_PIPELINE): a table entry is a dependent load (digit ->
+// address) from L2 / Infinity Cache / HBM, so each addition starts the fetch of the NEXT addition's
+// entry as soon as it has read its own: `st.stage(row, d)` starts fetching entry d of a row into the
+// lane's staging buffer (on the device: LDS-DMA, no VGPRs held while in flight), `st.staged(part, w)`
+// reads part of the staged entry back (A: halves of 20 words; B: 20 words, then 10). The fetch of
+// entry i - 1 is in flight during the last two multiplications of addition i and its p1p1 -> p3.
+#ifndef PV_COMB_PIPELINE
+#define PV_COMB_PIPELINE 1
+#endif
+template <class BStage, class Dig>
+PV_HD void pv_comb_b_acc_staged(ge_p3& acc, const BStage& st, const Dig& dig) {
+    ge_p3_identity(acc);
+    ge_p1p1 t;
+    uint32_t fw = dig.fs(7);
+    int f = pv_half(fw, PV_BCOMB_POS - 1);
+    st.stage(PV_BCOMB_POS - 1, f < 0 ? -f : f);
+    for (int j = PV_BCOMB_POS - 1; j >= 0; j--) {
+        const bool neg = f < 0;
+        uint32_t w[20];
+        st.staged(0, w);
+        fe ypx, ymx, xy2d, tt, a, b, c, d;
+        pv_sel_pm(ypx, ymx, w, neg);
+        if (j > 0 && (j & 1) == 0) fw = dig.fs((j - 1) >> 1);  // lands during the two products
+        fe_sub(tt, acc.Y, acc.X);
+        fe_mul(a, tt, ymx);
+        fe_add(tt, acc.Y, acc.X);
+        fe_mul(b, tt, ypx);
+        st.staged(1, w);
+#pragma unroll
+        for (int i = 0; i < 10; i++) xy2d.v[i] = w[i];
+        if (j > 0) {
+            f = pv_half(fw, j - 1);
+            st.stage(j - 1, f < 0 ? -f : f);
+        }
+        fe_cneg(xy2d, xy2d, neg);
+        fe_mul(c, acc.T, xy2d);
+        fe_add(d, acc.Z, acc.Z);  // 2 Z, not carried (see ge_add_niels)
+        fe_sub(t.X, b, a);
+        fe_add(t.Y, b, a);
+        fe_add(t.Z, d, c);
+        fe_sub(t.T, d, c);
+        ge_niels_p1p1_to_p3(acc, t);
+    }
+}
+
+template <class AStage, class Dig>
+PV_HD void pv_comb_a_xyz_staged(fe& X, fe& Y, fe& Z, const ge_p3& accB, const AStage& st, const Dig& dig) {
+    ge_p3 acc = accB;
+    ge_p1p1 t;
+    uint32_t ew = dig.ek(7);
+    int e = pv_byte(ew, PV_COMB_POS - 1);
+    st.stage(PV_COMB_POS - 1, e < 0 ? -e : e);
+    for (int i = PV_COMB_POS - 1; i >= 0; i--) {
+        const bool neg = e < 0;
+        uint32_t w[20];
+        st.staged(0, w);
+        fe ypx, ymx, tt, a, b, c, d, z2, t2d;
+        pv_sel_pm(ypx, ymx, w, neg);
+        if (i > 0 && (i & 3) == 0) ew = dig.ek((i - 1) >> 2);  // lands during the two products
+        fe_sub(tt, acc.Y, acc.X);
+        fe_mul(a, tt, ymx);
+        fe_add(tt, acc.Y, acc.X);
+        fe_mul(b, tt, ypx);
+        st.staged(1, w);
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            z2.v[q] = w[q];
+            t2d.v[q] = w[10 + q];
+        }
+        if (i > 0) {
+            e = pv_byte(ew, i - 1);
+            st.stage(i - 1, e < 0 ? -e : e);
+        }
+        fe_cneg(t2d, t2d, neg);
+        fe_mul(c, acc.T, t2d);
+        fe_mul(d, acc.Z, z2);
+        fe_sub(t.X, b, a);
+        fe_add(t.Y, b, a);
+        fe_add(t.Z, d, c);
+        fe_sub(t.T, d, c);
+        if (i > 0) {
+            ge_p1p1_to_p3(acc, t);
+        } else {
+            ge_p1p1_to_p2(X, Y, Z, t);
+        }
+    }
+}
+
+// Staging over plain Rows objects (host tests): stage() remembers the entry, staged() reads it.
+template <class ARows>
+struct PvRowsStageA {
+    const ARows& rows;
+    mutable int row_i, ent;
+    PV_HD void stage(int i, int d) const { row_i = i; ent = d; }
+    PV_HD void staged(int h, uint32_t w[20]) const { rows.row(row_i).load_half(ent, h, w); }
+};
+template <class BRows>
+struct PvRowsStageB {
+    const BRows& rows;
+    mutable int row_i, ent;
+    PV_HD void stage(int i, int d) const { row_i = i; ent = d; }
+    PV_HD void staged(int part, uint32_t w[20]) const { rows.row(row_i).load_part(ent, part, w); }
+};
+
 template <class BRows, class Dig>
 PV_HD void pv_comb_b_acc(ge_p3& acc, const BRows& brows, const Dig& dig) {
     ge_p3_identity(acc);
@@ -160,8 +270,13 @@ PV_HD void pv_comb_a_xyz(fe& X, fe& Y, fe& Z, const ge_p3& accB, const ARows& ar
 template <class ARows, class BRows, class Dig>
 PV_HD void pv_comb_xyz(fe& X, fe& Y, fe& Z, const ARows& arows, const BRows& brows, const Dig& dig) {
     ge_p3 acc;
+#if PV_COMB_PIPELINE
+    pv_comb_b_acc_staged(acc, PvRowsStageB<BRows>{brows, 0, 0}, dig);
+    pv_comb_a_xyz_staged(X, Y, Z, acc, PvRowsStageA<ARows>{arows, 0, 0}, dig);
+#else
     pv_comb_b_acc(acc, brows, dig);
     pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
+#endif
 }
 
 // ---------------------------------------------------------------- fixed-base comb (host, init)

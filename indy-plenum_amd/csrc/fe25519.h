@@ -10,9 +10,8 @@
 // v_mad_u64_u32 chain whose accumulator starts at the carry out of column k-1, so carrying costs
 // one v_lshrrev_b64 + one v_and_b32 per limb and no separate 64-bit adds. The wrapped products
 // use 19*g (computed once per operand by the caller when it is shared, fe_mul_pre) and odd x odd
-// products use 2*f. On the device every multiply-accumulate is an explicit v_mad_u64_u32 (inline
-// asm): left to itself the compiler widens a 32-bit operand whose top bit it cannot bound into a
-// 64 x 32 product (an extra mad + moves per term).
+// products use 2*f. Each column stays a single v_mad_u64_u32 chain on the device (PV_MAD_CHAIN
+// below).
 //
 // Bound discipline (asserted by the PV_BOUNDS_CHECK host build, tests/test_native_host.py):
 //   "R" reduced: limb < 2^width + 2^17. Output of fe_mul / fe_sq / fe_carry.
@@ -65,13 +64,37 @@ PV_HD void fe_check_reduced(const fe& f) {
 
 // ------------------------------------------------------------------ VALU primitives
 // acc + a*b (64-bit) and a*b: one v_mad_u64_u32 each on the device.
-PV_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
+// PV_MAD_CHAIN: each product-scanning column stays ONE chain of v_mad_u64_u32 (the accumulator of
+// every mad is the previous mad's result). Left alone, the compiler re-associates a column into two
+// chains joined by a v_lshl_add_u64 (one extra 4-cycle VOP3 per column, ~80 per point addition); an
+// empty non-volatile asm on each partial sum hides the algebra from it without emitting anything or
+// constraining the schedule beyond the data dependence. (PV_MAD_ASM: the mad itself as inline asm,
+// kept for comparison: hipcc then pads the opaque instructions with hazard s_nops.)
+#ifndef PV_MAD_CHAIN
+#define PV_MAD_CHAIN 1
+#endif
+#ifndef PV_MAD_ASM
+#define PV_MAD_ASM 0
+#endif
+PV_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__) && PV_MAD_ASM
+    uint64_t r, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(r), "=s"(cc) : "v"(a), "v"(b), "v"(c));
+    return r;
+#elif defined(__HIP_DEVICE_COMPILE__) && PV_MAD_CHAIN
+    uint64_t r = (uint64_t)a * b + c;
+    asm("" : "+v"(r));
+    return r;
+#else
+    return (uint64_t)a * b + c;
+#endif
+}
 PV_HD uint64_t mul64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
 // Opaque copy: stops the compiler from re-associating a column sum so that the carry from the
 // previous column is added by a separate v_lshl_add_u64 instead of entering the first
 // v_mad_u64_u32 of the column as its accumulator (no instruction is emitted).
 PV_HD uint64_t pv_opaque64(uint64_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !PV_MAD_ASM && !PV_MAD_CHAIN
     asm volatile("" : "+v"(x));
 #endif
     return x;

@@ -68,6 +68,8 @@ PV_HD void ge_p1p1_to_p2(fe& X, fe& Y, fe& Z, const ge_p1p1& p) {
     pv_sched_fence();
 }
 
+// X3 = X T, Z3 = Z T, Y3 = Z Y, T3 = X Y: two g operands (T, Y), so 19 g is formed twice, not 3 times
+// (every p1p1 limb here is < 3 * 2^26 + 2^18 < PV_GMAX, a valid g operand).
 PV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
     uint32_t g19[10];
     fe_mul19(g19, p.T);
@@ -75,10 +77,11 @@ PV_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
     pv_sched_fence();
     fe_mul_pre(r.Z, p.Z, p.T, g19);
     pv_sched_fence();
-    fe_mul19(g19, p.Z);
-    fe_mul_pre(r.Y, p.Y, p.Z, g19);
+    fe_mul19(g19, p.Y);
+    fe_mul_pre(r.Y, p.Z, p.Y, g19);
     pv_sched_fence();
-    fe_mul(r.T, p.X, p.Y);
+    fe_mul_pre(r.T, p.X, p.Y, g19);
+    pv_sched_fence();
 }
 
 // r = p + q  (q cached, possibly negated by the caller; p in R). Output limbs < 3 * 2^w + 2^18.

@@ -213,6 +213,9 @@ struct KeyWork {
     uint32_t seed;
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
+// key_count / key_cursor hold one counter per 64 B: every request bumps its key's counter, and with
+// 1,024 keys packed 32 to a cache line the atomics of a 1M-request chunk queued on 32 lines of L2
+static constexpr uint32_t PV_CNT_PAD = 16;
 
 // Kernel 1: checks, decompression of A, k = SHA-512(R||A||M) mod L, table of [j](-A), recoding.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __restrict__ sm,
@@ -338,7 +341,10 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* 
     pv_load_pk(A, pk, i);
     uint32_t h = pv_key_hash(A, kw.seed) & kw.hmask;
     for (uint32_t probe = 0; probe <= kw.hmask; probe++) {  // the table is >= 2x the chunk: never full
-        const uint32_t cur = atomicCAS(&kw.slot[h], PV_EMPTY, i);
+        // a plain read first: once a key is in, its other requests find it without an atomic (the
+        // atomics of one key's requests all queue on one slot)
+        uint32_t cur = __hip_atomic_load(&kw.slot[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == PV_EMPTY) cur = atomicCAS(&kw.slot[h], PV_EMPTY, i);
         if (cur == PV_EMPTY) break;
         uint32_t B[8];
         pv_load_pk(B, pk, cur);
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_count_kernel(uint64_t n, KeyW
     if (i >= n || *kw.nkeys > kw.kcap) return;  // over capacity: the Straus path runs, ids unused
     const uint32_t id = kw.slot_id[kw.req_key[i]];
     kw.req_key[i] = id;
-    atomicAdd(&kw.key_count[id], 1u);
+    atomicAdd(&kw.key_count[id * PV_CNT_PAD], 1u);
 }
 
 // Sort 2/3: exclusive prefix sum of key_count into key_cursor (one workgroup; nkeys <= kcap).
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
     uint32_t sum = 0;
     for (uint32_t j = 0; j < per; j++) {
         const uint32_t id = t * per + j;
-        if (id < nk) sum += kw.key_count[id];
+        if (id < nk) sum += kw.key_count[id * PV_CNT_PAD];
     }
     part[t] = sum;
     __syncthreads();
@@ -394,8 +400,8 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
     for (uint32_t j = 0; j < per; j++) {
         const uint32_t id = t * per + j;
         if (id < nk) {
-            kw.key_cursor[id] = base;
-            base += kw.key_count[id];
+            kw.key_cursor[id * PV_CNT_PAD] = base;
+            base += kw.key_count[id * PV_CNT_PAD];
         }
     }
 }
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_scatter_kernel(uint64_t n, Ke
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t id = kw.req_key[i];
-    const uint32_t pos = atomicAdd(&kw.key_cursor[id], 1u);
+    const uint32_t pos = atomicAdd(&kw.key_cursor[id * PV_CNT_PAD], 1u);
     kw.slot_req[pos] = i;
     kw.req_pos[i] = pos;
     kw.skey[pos] = id;
@@ -505,6 +511,60 @@ struct DevBRows {
     const uint4* base;
     __device__ __forceinline__ DevBRow row(int i) const {
         return DevBRow{base + (uint32_t)i * PV_BCOMB_ENT * (PV_BCOMB_STRIDE / 4)};
+    }
+};
+
+// LDS-DMA staging of one table entry per lane (comb.h, PV_COMB_PIPELINE). An entry of Q uint4 is
+// fetched by Q global_load_lds_dwordx4, each writing 1 KiB = 16 B x 64 lanes of the wave's staging
+// area, laid out [q][lane] so that reading it back is one conflict-free ds_read_b128 per q.
+__device__ __forceinline__ void pv_glds16(const uint4* g, uint4* l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+// the LDS reads of the previous staged entry must be complete before its buffer is refilled
+__device__ __forceinline__ void pv_lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+struct DevCombStage {  // per-key comb table rows, entries of 10 uint4
+    const uint4* key;  // the key's table [32][129][10]
+    uint4* lds;        // this wave's [10][64] staging area
+    uint32_t lane;
+    __device__ __forceinline__ void stage(int i, int d) const {
+        const uint4* e = key + ((uint32_t)i * PV_COMB_ENT + (uint32_t)d) * 10;
+        pv_lds_reads_done();
+#pragma unroll
+        for (int q = 0; q < 10; q++) pv_glds16(e + q, lds + q * 64);
+    }
+    __device__ __forceinline__ void staged(int h, uint32_t w[20]) const {
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const uint4 v = lds[(5 * h + q) * 64 + lane];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+    }
+};
+struct DevBStage {  // fixed-base comb rows, entries of PV_BCOMB_STRIDE words (8 uint4, 30 words used)
+    const uint4* base;  // T_B [16][32769][8]
+    uint4* lds;         // this wave's [8][64] staging area
+    uint32_t lane;
+    __device__ __forceinline__ void stage(int j, int d) const {
+        const uint4* e = base + ((uint32_t)j * PV_BCOMB_ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4);
+        pv_lds_reads_done();
+#pragma unroll
+        for (int q = 0; q < PV_BCOMB_STRIDE / 4; q++) pv_glds16(e + q, lds + q * 64);
+    }
+    __device__ __forceinline__ void staged(int part, uint32_t w[20]) const {
+#pragma unroll
+        for (int q = 0; q < (part ? 3 : 5); q++) {
+            const uint4 v = lds[(5 * part + q) * 64 + lane];
+            const int lim = part ? 10 : 20;
+            if (4 * q < lim) w[4 * q] = v.x;
+            if (4 * q + 1 < lim) w[4 * q + 1] = v.y;
+            if (4 * q + 2 < lim) w[4 * q + 2] = v.z;
+            if (4 * q + 3 < lim) w[4 * q + 3] = v.w;
+        }
     }
 };
 
@@ -680,7 +740,13 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
     if (i >= n) return;
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     ge_p3 acc;
+#if PV_COMB_PIPELINE
+    __shared__ uint4 stg[PV_BLOCK / 64][PV_BCOMB_STRIDE / 4][64];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    pv_comb_b_acc_staged(acc, DevBStage{bcomb, &stg[wv][0][0], threadIdx.x & 63u}, dig);
+#else
     pv_comb_b_acc(acc, DevBRows{bcomb}, dig);
+#endif
     const Soa qs(wk.q, 40, wk.stride);
 #pragma unroll
     for (int q = 0; q < 10; q++) {
@@ -691,12 +757,29 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
     }
 }
 
+// XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs (block b runs on the XCD
+// of b % 8; MI355X_MICROARCH.md, workgroup dispatch), each XCD with its own 4 MB L2. Slot order is
+// key-sorted, so mapping the blocks of XCD x to ONE contiguous range of slots keeps a key's table
+// rows in one L2 instead of fetching them into all eight. A bijection on [0, gridDim.x).
+#ifndef PV_XCD_REMAP
+#define PV_XCD_REMAP 1
+#endif
+__device__ __forceinline__ uint32_t pv_xcd_block() {
+#if PV_XCD_REMAP
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+    return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+#else
+    return blockIdx.x;
+#endif
+}
+
 // Second half: Q = acc + [k](-A) from the key's comb table (32 additions, no doublings), projective
 // Q to q rows 0..29; the key's own libsodium checks are folded into flags[i] here.
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                Gate gate) {
     if (!gate.comb()) return;
-    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
+    const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
     if (i >= n) return;
     const uint32_t id = kw.skey[i];
     const uint32_t S = (uint32_t)wk.stride;
@@ -709,10 +792,19 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
         acc.Z.v[q] = qs.ld(20 + q, i);
         acc.T.v[q] = qs.ld(30 + q, i);
     }
-    const DevCombRows arows{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10};
     const DevDigits dig{wk.digits, S, i};
     fe X, Y, Z;
+#if PV_COMB_PIPELINE
+    __shared__ uint4 stg[PV_BLOCK / 64][10][64];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    pv_comb_a_xyz_staged(X, Y, Z, acc,
+                         DevCombStage{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10, &stg[wv][0][0],
+                                      threadIdx.x & 63u},
+                         dig);
+#else
+    const DevCombRows arows{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10};
     pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
+#endif
     if (kw.key_flag[id] == 0) wk.flags[i] = 0;
 #pragma unroll
     for (int q = 0; q < 10; q++) {
@@ -911,7 +1003,7 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             gate = Gate{kw.nkeys, limit};
             // key-sorted slot order for the per-request comb kernels
-            PV_HIP(hipMemsetAsync(kw.key_count, 0, (uint64_t)kw.kcap * 4, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipMemsetAsync(kw.key_count, 0, (uint64_t)kw.kcap * PV_CNT_PAD * 4, stream), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_count_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(1024), 0, stream, kw);
@@ -941,26 +1033,34 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
                            d_pk + 32 * c0, g_ctx.work, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         if (limit > 0) {
+            // The Straus kernels go first: when the gate picks the comb path they exit at their first
+            // instruction, and here, with only the few key-chain waves resident, their 4,096
+            // workgroups drain in microseconds. Launched between the comb kernels instead, the gated
+            // table kernel waited ~170 us for CUs held by the table fill (round-1 trace).
+            hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+                               g_ctx.d_btab, g_ctx.work, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, g_ctx.kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        }
-        if ((rc = mark(PV_STAGE_TABLE))) return rc;
-        hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
-        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (limit > 0) {
+            if ((rc = mark(PV_STAGE_TABLE))) return rc;
             // [S]B while the key stream finishes the tables, then join
             hipLaunchKernelGGL(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bcomb,
                                gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
-        }
-        if ((rc = mark(PV_STAGE_MSM))) return rc;
-        hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                           g_ctx.d_btab, g_ctx.work, gate);
-        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (limit > 0) {
+            if ((rc = mark(PV_STAGE_MSM))) return rc;
             hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.kw, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        } else {
+            if ((rc = mark(PV_STAGE_TABLE))) return rc;
+            hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            if ((rc = mark(PV_STAGE_MSM))) return rc;
+            hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+                               g_ctx.d_btab, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         }
         if ((rc = mark(PV_STAGE_ENCODE))) return rc;
@@ -1037,8 +1137,8 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * 160), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_count, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_cursor, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_count, (uint64_t)kw.kcap * PV_CNT_PAD * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_cursor, (uint64_t)kw.kcap * PV_CNT_PAD * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.slot_req, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_pos, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.skey, S * 4), PV_ERR_ALLOC);

@@ -24,6 +24,7 @@ def dalloc(b):
 d_blob = dalloc(blob.nbytes + 256); d_off = dalloc(off.nbytes); d_pk = dalloc(pks.nbytes); d_v = dalloc((n + 63) // 64 * 8)
 L.pv_memcpy_h2d(d_blob, blob.ctypes.data, blob.nbytes); L.pv_memcpy_h2d(d_off, off.ctypes.data, off.nbytes); L.pv_memcpy_h2d(d_pk, pks.ctypes.data, pks.nbytes)
 L.pv_set_timing(1)
+rows = []
 for it in range(int(os.environ.get("IT", "3"))):
     t = time.time()
     _native.check(L.pv_verify_batch_device(d_blob, d_off, n, d_pk, d_v, None), "verify")
@@ -33,5 +34,12 @@ for it in range(int(os.environ.get("IT", "3"))):
     L.pv_stage_times(st, 5, ctypes.byref(nl)); L.pv_set_timing(1)
     v = np.zeros((n + 63) // 64, np.uint64); L.pv_memcpy_d2h(v.ctypes.data, d_v, v.nbytes)
     ok = int(np.unpackbits(v.view(np.uint8), bitorder="little")[:n].sum())
-    print({"n": n, "wall_s": round(dt, 4), "verifies_per_s": round(n / dt),
-           **{k + "_ms": round(v, 3) for k, v in zip(_native.PV_STAGES, st)}, "valid": ok}, flush=True)
+    row = {"n": n, "wall_s": round(dt, 4), "verifies_per_s": round(n / dt),
+           **{k + "_ms": round(v, 3) for k, v in zip(_native.PV_STAGES, st)}, "valid": ok}
+    rows.append(row)
+    if os.environ.get("VERBOSE"):
+        print(row, flush=True)
+tail = rows[min(3, len(rows) - 1):]
+med = {k: float(np.median([r[k] for r in tail])) for k in tail[0] if k.endswith("_ms")}
+print({"lib": os.path.basename(_native.LIB_PATH), "iters": len(tail), "valid": rows[-1]["valid"],
+       "sum_ms": round(sum(med.values()), 4), **{k: round(v, 4) for k, v in med.items()}}, flush=True)
