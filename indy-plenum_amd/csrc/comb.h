@@ -13,7 +13,7 @@
 // i.e. 48 point additions and NO doublings (the Straus path needs 252 doublings + 96 additions).
 // The encoding / comparison with R is unchanged (pv_encode_batch), so the verdict is the same
 // function of (R, S, A, M) as libsodium's crypto_sign_open (stp_core/crypto/nacl_wrappers.py:108).
-// Per-key work: one decompression, 248 doublings (the chain of bases [256^i](-A)), 4,128 additions.
+// Per-key work: one decompression, 254 doublings (the chain of bases [256^i](-A)), ~4,130 additions.
 #pragma once
 #include "btable.h"
 #include "verify_core.h"
@@ -26,29 +26,45 @@ static constexpr int PV_BCOMB_POS = 16;       // radix-65536 digit positions of 
 static constexpr int PV_BCOMB_ENT = 32769;    // entries per position (|digit| = 0..32768)
 
 // ---------------------------------------------------------------- per-key expansion
-// bases[i] = [256^i](-A) as extended points, i = 0..31: 31 x (7 doublings to p2 + 1 to p3).
+// Points kept per position i (P_i = [256^i](-A)) for the table fill: slot 0 = P_i, slots 1..3 =
+// [16] P_i, [32] P_i, [64] P_i -- the chain passes through them on its way to P_{i+1}.
+static constexpr int PV_COMB_PTS = 4;
+
+// out.store(i, m, p): slot m of position i. 31 x 8 doublings (the last position only 6, to reach
+// [64] P_31); a doubling whose result is stored or continues the chain as P_{i+1} also forms T.
 template <class Bases>
 PV_HD void pv_comb_chain(const Bases& out, const ge_p3& negA) {
     ge_p3 cur = negA;
-    out.store(0, cur);
-    for (int i = 1; i < PV_COMB_POS; i++) {
-        ge_p1p1 t;
+    for (int i = 0; i < PV_COMB_POS; i++) {
+        out.store(i, 0, cur);
         fe X = cur.X, Y = cur.Y, Z = cur.Z;
-        for (int j = 0; j < 7; j++) {
+        const int nd = i + 1 < PV_COMB_POS ? 8 : 6;
+        for (int j = 0; j < nd; j++) {
+            ge_p1p1 t;
             ge_p2_dbl(t, X, Y, Z);
-            ge_p1p1_to_p2(X, Y, Z, t);
+            if ((j >= 3 && j <= 5) || j == 7) {
+                ge_p3 q;
+                ge_p1p1_to_p3(q, t);
+                if (j <= 5) out.store(i, j - 2, q);
+                else cur = q;
+                X = q.X;
+                Y = q.Y;
+                Z = q.Z;
+            } else {
+                ge_p1p1_to_p2(X, Y, Z, t);
+            }
         }
-        ge_p2_dbl(t, X, Y, Z);
-        ge_p1p1_to_p3(cur, t);
-        out.store(i, cur);
     }
 }
 
 // Entries d = 16 b + 1 .. 16 b + 16 of one position (block b = 0..7; block 0 also writes the
-// identity at d = 0) from the position's base P: start at [16 b] P by double-and-add, then 16
+// identity at d = 0). pts.load(m, p) gives slot m of the position (see pv_comb_chain). The start
+// point [16 b] P is a sum of the chain's [16] P, [32] P, [64] P (at most two additions), then 16
 // additions of P.
-template <class Table>
-PV_HD void pv_comb_fill_block(const Table& tab, const ge_p3& P, int b) {
+template <class Table, class Pts>
+PV_HD void pv_comb_fill_block(const Table& tab, const Pts& pts, int b) {
+    ge_p3 P;
+    pts.load(0, P);
     ge_cached cP;
     ge_p3_to_cached(cP, P);
     ge_p3 cur;
@@ -59,24 +75,18 @@ PV_HD void pv_comb_fill_block(const Table& tab, const ge_p3& P, int b) {
         tab.store(0, id);
         ge_p3_identity(cur);
     } else {
-        // [b] P for b = 1..7 (top bit first), then 4 doublings -> [16 b] P
-        cur = P;
         const int top = b >= 4 ? 2 : (b >= 2 ? 1 : 0);
+        pts.load(1 + top, cur);
         for (int bit = top - 1; bit >= 0; bit--) {
-            ge_p2_dbl(t, cur.X, cur.Y, cur.Z);
-            ge_p1p1_to_p3(cur, t);
             if ((b >> bit) & 1) {
-                ge_add_cached(t, cur, cP);
+                ge_p3 m;
+                pts.load(1 + bit, m);
+                ge_cached cm;
+                ge_p3_to_cached(cm, m);
+                ge_add_cached(t, cur, cm);
                 ge_p1p1_to_p3(cur, t);
             }
         }
-        fe X = cur.X, Y = cur.Y, Z = cur.Z;
-        for (int j = 0; j < 3; j++) {
-            ge_p2_dbl(t, X, Y, Z);
-            ge_p1p1_to_p2(X, Y, Z, t);
-        }
-        ge_p2_dbl(t, X, Y, Z);
-        ge_p1p1_to_p3(cur, t);
     }
     for (int d = 16 * b + 1; d <= 16 * b + 16; d++) {
         ge_add_cached(t, cur, cP);

@@ -185,7 +185,7 @@ struct Gate {
 //   nkeys    [1]       distinct keys counted
 //   key_owner[kcap]    a request carrying key id
 //   key_flag [kcap]    libsodium key checks passed (canonical, not small-order, decompresses)
-//   bases    [kcap][32][10] uint4    [256^i](-A), extended
+//   bases    [kcap][32][4][10] uint4 [256^i](-A) and its [16], [32], [64] multiples, extended
 //   ctab     [kcap][32][129][10] uint4  T_A, cached form
 // Key-sorted processing order ("slots"): after dedup the requests of each key occupy a contiguous
 // range of slots, so consecutive lanes and waves read the same key's table rows (L2-resident)
@@ -433,8 +433,8 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_unpermute_kernel(uint64_t n, KeyW
 }
 
 struct DevBases {
-    uint4* b;  // [32][10]
-    __device__ __forceinline__ void store(int i, const ge_p3& p) const {
+    uint4* b;  // [32][PV_COMB_PTS][10]: per position P_i, [16] P_i, [32] P_i, [64] P_i (extended)
+    __device__ __forceinline__ void store(int i, int m, const ge_p3& p) const {
         uint32_t w[40];
 #pragma unroll
         for (int q = 0; q < 10; q++) {
@@ -443,14 +443,16 @@ struct DevBases {
             w[20 + q] = p.Z.v[q];
             w[30 + q] = p.T.v[q];
         }
+        uint4* e = b + (i * PV_COMB_PTS + m) * 10;
 #pragma unroll
-        for (int q = 0; q < 10; q++) b[i * 10 + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        for (int q = 0; q < 10; q++) e[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
     }
-    __device__ __forceinline__ void load(int i, ge_p3& p) const {
+    __device__ __forceinline__ void load(int i, int m, ge_p3& p) const {
+        const uint4* e = b + (i * PV_COMB_PTS + m) * 10;
         uint32_t w[40];
 #pragma unroll
         for (int q = 0; q < 10; q++) {
-            const uint4 v = b[i * 10 + q];
+            const uint4 v = e[q];
             w[4 * q] = v.x;
             w[4 * q + 1] = v.y;
             w[4 * q + 2] = v.z;
@@ -464,6 +466,11 @@ struct DevBases {
             p.T.v[q] = w[30 + q];
         }
     }
+};
+struct DevBasePts {  // the points of one position, for pv_comb_fill_block
+    DevBases bs;
+    int i;
+    __device__ __forceinline__ void load(int m, ge_p3& p) const { bs.load(i, m, p); }
 };
 
 // One position's row of a key's comb table: entries d = 0..128, 10 uint4 (160 B) each.
@@ -580,7 +587,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_kernel(const uint8_t
     ge_p3 negA;
     const bool ok = pv_key_ok_negate(negA, A);
     kw.key_flag[id] = ok ? 1u : 0u;
-    pv_comb_chain(DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * 10}, negA);
+    pv_comb_chain(DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10}, negA);
 }
 
 // ---- quad-cooperative key chain: four lanes per key shorten the per-key critical path ~2x.
@@ -665,17 +672,23 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const ui
     ge_p3 cur;
     const bool ok = pv_key_ok_negate(cur, A);
     if (rl == 0) kw.key_flag[id] = ok ? 1u : 0u;
-    uint32_t* b = reinterpret_cast<uint32_t*>(kw.bases + (uint64_t)id * PV_COMB_POS * 10);
+    uint32_t* b = reinterpret_cast<uint32_t*>(kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10);
     fe X = cur.X, Y = cur.Y, Z = cur.Z, T = cur.T;
-    for (int i = 0; i < PV_COMB_POS; i++) {
-        if (i > 0) {
-            for (int j = 0; j < 8; j++) pv_quad_dbl(X, Y, Z, T, role, j == 7);
-        }
-        // lane r stores component r (X, Y, Z, T) of base i: words 10 r .. 10 r + 9
+    // lane r stores component r (X, Y, Z, T) of a point: words 10 r .. 10 r + 9 of its 40
+    auto store = [&](int i, int m) {
         fe mine;
         pv_fe_sel4(mine, X, Y, Z, T, role);
 #pragma unroll
-        for (int q = 0; q < 10; q++) b[i * 40 + 10 * rl + q] = mine.v[q];
+        for (int q = 0; q < 10; q++) b[(i * PV_COMB_PTS + m) * 40 + 10 * rl + q] = mine.v[q];
+    };
+    for (int i = 0; i < PV_COMB_POS; i++) {
+        store(i, 0);
+        // [2] .. [256] P_i; [16], [32], [64] P_i are kept for the table fill (pv_comb_chain)
+        const int nd = i + 1 < PV_COMB_POS ? 8 : 6;
+        for (int j = 0; j < nd; j++) {
+            pv_quad_dbl(X, Y, Z, T, role, (j >= 3 && j <= 5) || j == 7);
+            if (j >= 3 && j <= 5) store(i, j - 2);
+        }
     }
 }
 
@@ -687,9 +700,8 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_fill_kernel(KeyWork kw, Ga
         const uint32_t id = it / (PV_COMB_POS * PV_COMB_BLOCKS);
         const int pos = (it / PV_COMB_BLOCKS) % PV_COMB_POS;
         const int b = it % PV_COMB_BLOCKS;
-        ge_p3 P;
-        DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * 10}.load(pos, P);
-        pv_comb_fill_block(DevCombRow{kw.ctab + ((uint64_t)id * PV_COMB_POS + pos) * PV_COMB_ENT * 10}, P, b);
+        const DevBasePts pts{DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10}, pos};
+        pv_comb_fill_block(DevCombRow{kw.ctab + ((uint64_t)id * PV_COMB_POS + pos) * PV_COMB_ENT * 10}, pts, b);
     }
 }
 
@@ -1135,7 +1147,7 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.nkeys, 256), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_owner, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * 160), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_PTS * 160), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_count, (uint64_t)kw.kcap * PV_CNT_PAD * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_cursor, (uint64_t)kw.kcap * PV_CNT_PAD * 4), PV_ERR_ALLOC);

@@ -97,8 +97,12 @@ int hc_enc_batch_size(void) { return PV_ENC_BATCH; }
 
 // ---- keyed comb path on the host (comb.h): same code the comb kernels run
 struct HostBases {
-    ge_p3* b;
-    void store(int i, const ge_p3& p) const { b[i] = p; }
+    ge_p3* b;  // [32][PV_COMB_PTS]
+    void store(int i, int m, const ge_p3& p) const { b[i * PV_COMB_PTS + m] = p; }
+};
+struct HostBasePts {
+    const ge_p3* b;  // the position's PV_COMB_PTS points
+    void load(int m, ge_p3& p) const { p = b[m]; }
 };
 struct HostCombRow {
     uint32_t* r;  // [129][40]
@@ -146,12 +150,13 @@ int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     ok &= pv_key_ok_negate(negA, in.A);
     uint32_t k[8];
     pv_hash_k(k, in, smlen, mw);
-    std::vector<ge_p3> bases(PV_COMB_POS);
+    std::vector<ge_p3> bases(PV_COMB_POS * PV_COMB_PTS);
     pv_comb_chain(HostBases{bases.data()}, negA);
     std::vector<uint32_t> ctab((size_t)PV_COMB_POS * PV_COMB_ENT * 40);
     for (int pos = 0; pos < PV_COMB_POS; pos++)
         for (int b = 0; b < PV_COMB_BLOCKS; b++)
-            pv_comb_fill_block(HostCombRow{ctab.data() + (size_t)pos * PV_COMB_ENT * 40}, bases[pos], b);
+            pv_comb_fill_block(HostCombRow{ctab.data() + (size_t)pos * PV_COMB_ENT * 40},
+                               HostBasePts{bases.data() + pos * PV_COMB_PTS}, b);
     pv_dig_regs dig;
     sc_recode256(dig.e, k);
     sc_recode65536(dig.f, in.S);

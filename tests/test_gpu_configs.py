@@ -175,3 +175,26 @@ def test_two_chunks_every_path(native, nym1m):
         got = native.verify_sm_batch(blob2, off2, pks2)
         native.set_path(native.PV_PATH_AUTO)
         assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
+
+
+def test_config5_shard_8M(native, nym1m):
+    """Config 5 (64M requests over 8 GPUs) as one GPU sees it: its 8M-request shard, 8 launch
+    chunks, each chunk deduplicating its keys and taking the comb path. Tiled from the 1M NYM set;
+    the 24 records corrupted across the chunks must be exactly the rejected ones."""
+    blob, off, pks = nym1m
+    reps = 8
+    n1, total = len(off) - 1, int(off[-1])
+    blob8 = np.tile(blob, reps)
+    off8 = np.concatenate([off[:-1] + np.uint64(r * total) for r in range(reps)]
+                          + [np.array([reps * total], np.uint64)]).astype(np.uint64)
+    pks8 = np.tile(pks, (reps, 1))
+    n = n1 * reps
+    bad = np.sort(np.random.default_rng(5).choice(n, 24, replace=False))
+    bad[0], bad[-1] = 0, n - 1
+    for i in bad:
+        blob8[int(off8[i]) + 70] ^= 0x20  # a message byte
+    want = np.ones(n, bool)
+    want[bad] = False
+    got = native.verify_sm_batch(blob8, off8, pks8)
+    assert len(got) == n
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
