@@ -98,18 +98,24 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
  *   PV_PATH_STRAUS  per request: decompress A, 9-entry table of [j](-A), regular-window Straus
  *                   double-scalar multiplication (252 doublings + 96 additions)
  *   PV_PATH_COMB    per batch: deduplicate keys; per DISTINCT key: decompress and expand a
- *                   radix-256 comb table; per request: 64 table additions, no doublings
- *                   (falls back to Straus when a chunk has more distinct keys than the tables hold)
- *   PV_PATH_AUTO    (default) comb when a chunk's distinct keys <= 0.021 n - 640 (from measured
- *                   per-key and per-request costs: large batches with repeated signers), else
- *                   Straus; decided on the device, so pv_verify_batch_device stays asynchronous. */
+ *                   radix-256 comb table; per request: 48 table additions, no doublings (keys
+ *                   beyond the PV_KEY_CAP = 16,384 tables a chunk holds take the Straus path)
+ *   PV_PATH_AUTO    (default) per chunk of >= 32,768 requests: deduplicate keys, give a comb table
+ *                   to every key with >= 48 requests in the chunk (a table costs about what ~50
+ *                   requests save) and verify the other requests on the Straus path in the same
+ *                   launch; smaller chunks go Straus. Split on the device, so
+ *                   pv_verify_batch_device stays asynchronous.
+ * Every path returns bit-identical verdicts. */
 #define PV_PATH_AUTO 0
 #define PV_PATH_STRAUS 1
 #define PV_PATH_COMB 2
 int pv_set_path(int mode);
-/* The path the most recent chunk took (PV_PATH_STRAUS or PV_PATH_COMB) and its distinct-key count
- * (0 when no key kernels ran). Synchronises the device. */
+/* The path the most recent chunk took (PV_PATH_COMB if any of its requests used a comb table, else
+ * PV_PATH_STRAUS) and its distinct-key count (0 when no key kernels ran). Synchronises the device. */
 int pv_last_path(int* path, uint32_t* nkeys);
+/* The split of the most recent chunk, as read by the last pv_last_path call: distinct keys, keys
+ * given a comb table, requests verified with those tables (the rest took the Straus path). */
+int pv_last_split(uint32_t* keys, uint32_t* comb_keys, uint32_t* comb_requests);
 int pv_set_timing(int enable);
 int pv_stage_times(double* ms, int max_stages, int* launches);
 int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* launches);

@@ -37,6 +37,7 @@ static constexpr int PV_BLOCK = 256;
 #endif
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
+static constexpr uint64_t PV_KEYED_MIN = 32768;   // AUTO: smaller chunks skip dedup (Straus only)
 
 // ---------------------------------------------------------------------------------------- device
 
@@ -167,38 +168,55 @@ struct Work {
     uint64_t stride;  // chunk capacity (requests)
 };
 
-// Which arithmetic path a chunk takes, decided ON THE DEVICE from the number of distinct keys the
-// dedup kernels counted (no host round trip): comb iff nkeys <= limit. nkeys == nullptr means
-// the Straus path was forced and no key kernels ran.
+// How a chunk's requests are split between the two arithmetic paths, decided ON THE DEVICE by the
+// dedup/sort kernels (no host round trip). split == nullptr: the Straus path was forced (or the
+// chunk is too small for dedup to pay) -- no key kernels ran and slot == request. Otherwise the
+// requests are in key-sorted slot order, the first split[PV_SPLIT_SLOTS] slots belong to keys
+// that take the comb path and the remaining slots take the Straus path (request = slot_req[slot]).
+static constexpr int PV_SPLIT_KEYS = 0;        // distinct keys in the chunk
+static constexpr int PV_SPLIT_COMB_KEYS = 1;   // keys given a comb table
+static constexpr int PV_SPLIT_SLOTS = 2;       // requests (slots) of those keys
 struct Gate {
-    const uint32_t* nkeys;
-    uint32_t limit;
-    __device__ __forceinline__ bool comb() const { return nkeys && *nkeys <= limit; }
-    __device__ __forceinline__ bool straus() const { return !comb(); }
+    const uint32_t* split;
+    const uint32_t* slot_req;
+    __device__ __forceinline__ bool keyed() const { return split != nullptr; }
+    // block of a Straus-path kernel: from the end of the slot range when split (the Straus slots
+    // are the last ones, so the blocks with work are dispatched first)
+    __device__ __forceinline__ uint32_t sblock() const { return split ? gridDim.x - 1 - blockIdx.x : blockIdx.x; }
+    __device__ __forceinline__ uint32_t ncomb() const { return split ? split[PV_SPLIT_SLOTS] : 0u; }
+    // request of a Straus-path slot
+    __device__ __forceinline__ uint32_t req(uint32_t i) const { return split ? slot_req[i] : i; }
 };
 
-// Keyed comb workspace (comb.h). The hash table maps a 32-byte key to the index of the first
-// request that carried it; slot_id gives the dense key id of an owned slot.
+// Keyed workspace (comb.h). The hash table maps a 32-byte key to the index of the first request
+// that carried it; slot_id gives the dense key id of an owned slot (ids < chunk size).
 //   slot     [H] u32   owner request index, PV_EMPTY = free
 //   slot_id  [H] u32   dense key id of an owned slot
-//   req_key  [stride]  the request's slot, then (after pv_key_assign) its key id
-//   nkeys    [1]       distinct keys counted
-//   key_owner[kcap]    a request carrying key id
-//   key_flag [kcap]    libsodium key checks passed (canonical, not small-order, decompresses)
+//   req_key  [stride]  the request's slot, then (after pv_key_count) its key id
+//   nkeys    [3]       PV_SPLIT_* counters (see Gate)
+//   key_owner[stride]  a request carrying key id
+//   key_cid  [stride]  comb index of key id (PV_EMPTY: its requests take the Straus path)
+//   comb_key [kcap]    key id of comb index j;  key_flag [kcap]  libsodium key checks passed
 //   bases    [kcap][32][4][10] uint4 [256^i](-A) and its [16], [32], [64] multiples, extended
 //   ctab     [kcap][32][129][10] uint4  T_A, cached form
+// A key takes the comb path when it carries >= min_req requests of the chunk (the per-key table
+// costs about as much as ~50 requests save; 1 when the comb path is forced) and fewer than kcap
+// keys came before it; the rest -- singletons such as the adversarial keys of config 3 -- take the
+// Straus path in the same launch.
 // Key-sorted processing order ("slots"): after dedup the requests of each key occupy a contiguous
-// range of slots, so consecutive lanes and waves read the same key's table rows (L2-resident)
-// instead of 1,024 keys' tables at random. Per-request kernels of the comb path run in slot order:
-//   key_count[kcap], key_cursor[kcap]   requests per key, then the next free slot of each key
+// range of slots, comb keys first, so consecutive lanes and waves read the same key's table rows
+// (L2-resident) instead of 1,024 keys' tables at random:
+//   key_count[stride], key_cursor[stride]  requests per key, then the next free slot of each key
 //   slot_req [stride]                   slot -> request index;  req_pos [stride] request -> slot
-//   skey     [stride]                   slot -> key id;         sverdict [stride / 64] slot verdicts
+//   skey     [stride]                   slot -> comb index;     sverdict [stride / 64] slot verdicts
 struct KeyWork {
     uint32_t* slot;
     uint32_t* slot_id;
     uint32_t* req_key;
     uint32_t* nkeys;
     uint32_t* key_owner;
+    uint32_t* key_cid;
+    uint32_t* comb_key;
     uint32_t* key_flag;
     uint4* bases;
     uint4* ctab;
@@ -211,20 +229,26 @@ struct KeyWork {
     uint32_t hmask;
     uint32_t kcap;
     uint32_t seed;
+    uint32_t min_req;
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 // key_count / key_cursor hold one counter per 64 B: every request bumps its key's counter, and with
 // 1,024 keys packed 32 to a cache line the atomics of a 1M-request chunk queued on 32 lines of L2
 static constexpr uint32_t PV_CNT_PAD = 16;
+#ifndef PV_COMB_MIN_REQ
+#define PV_COMB_MIN_REQ 48
+#endif
 
 // Kernel 1: checks, decompression of A, k = SHA-512(R||A||M) mod L, table of [j](-A), recoding.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __restrict__ sm,
                                                                const uint64_t* __restrict__ off, uint64_t n,
                                                                const uint8_t* __restrict__ pk, Work wk, Gate gate) {
-    if (!gate.straus()) return;
-    const uint64_t i = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t o0 = off[i], o1 = off[i + 1];
+    const uint32_t nc = gate.ncomb(), sb = gate.sblock();
+    if ((sb + 1) * PV_BLOCK <= nc) return;  // a block of comb-path slots
+    const uint64_t i = (uint64_t)sb * PV_BLOCK + threadIdx.x;  // slot
+    if (i >= n || i < nc) return;
+    const uint32_t r = gate.req((uint32_t)i);                          // request
+    const uint64_t o0 = off[r], o1 = off[r + 1];
     const uint64_t smlen = o1 - o0;
     const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
     const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
@@ -234,7 +258,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __r
         in.R[q] = mw.dw(q);
         in.S[q] = mw.dw(8 + q);
     }
-    const uint4* pk4 = reinterpret_cast<const uint4*>(pk + 32 * i);
+    const uint4* pk4 = reinterpret_cast<const uint4*>(pk + 32 * (uint64_t)r);
     const uint4 a0 = pk4[0], a1 = pk4[1];
     in.A[0] = a0.x; in.A[1] = a0.y; in.A[2] = a0.z; in.A[3] = a0.w;
     in.A[4] = a1.x; in.A[5] = a1.y; in.A[6] = a1.z; in.A[7] = a1.w;
@@ -267,9 +291,10 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __r
 
 // Kernel 1b: expand -A (extended, in slot 1) into the cached table [j](-A), j = 0..8.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk, Gate gate) {
-    if (!gate.straus()) return;
-    const uint64_t i = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
-    if (i >= n) return;
+    const uint32_t nc = gate.ncomb(), sb = gate.sblock();
+    if ((sb + 1) * PV_BLOCK <= nc) return;
+    const uint64_t i = (uint64_t)sb * PV_BLOCK + threadIdx.x;  // slot
+    if (i >= n || i < nc) return;
     const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
     uint32_t w[40];
     at.load(1, w);
@@ -289,14 +314,15 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
                                                               const uint64_t* __restrict__ off, uint64_t n,
                                                               const uint32_t* __restrict__ btab_g, Work wk,
                                                               Gate gate) {
-    if (!gate.straus()) return;
+    const uint32_t nc = gate.ncomb(), sb = gate.sblock();
+    if ((sb + 1) * PV_BLOCK <= nc) return;  // a block of comb-path slots (before the LDS fill)
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
     for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
         reinterpret_cast<uint4*>(sbt)[t] = reinterpret_cast<const uint4*>(btab_g)[t];
     __syncthreads();
-    const uint64_t i0 = (uint64_t)blockIdx.x * PV_BLOCK + threadIdx.x;
-    const bool active = i0 < n;
-    const uint64_t i = active ? i0 : n - 1;
+    const uint64_t i0 = (uint64_t)sb * PV_BLOCK + threadIdx.x;  // slot
+    const bool active = i0 < n && i0 >= nc;
+    const uint64_t i = active ? i0 : n - 1;  // n - 1 >= nc here: a Straus slot
     const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
     const LdsBTab bt{sbt};
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, (uint32_t)i};
@@ -360,68 +386,94 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, Key
     if (i >= n) return;
     const uint32_t s = kw.req_key[i];
     if (kw.slot[s] != i) return;
-    const uint32_t id = atomicAdd(kw.nkeys, 1u);
-    if (id < kw.kcap) {
-        kw.slot_id[s] = id;
-        kw.key_owner[id] = i;
-    }
+    const uint32_t id = atomicAdd(&kw.nkeys[PV_SPLIT_KEYS], 1u);  // < n
+    kw.slot_id[s] = id;
+    kw.key_owner[id] = i;
 }
 
 // Sort 1/3: dense key id per request (req_key: slot -> id) and requests per key.
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_count_kernel(uint64_t n, KeyWork kw) {
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
-    if (i >= n || *kw.nkeys > kw.kcap) return;  // over capacity: the Straus path runs, ids unused
+    if (i >= n) return;
     const uint32_t id = kw.slot_id[kw.req_key[i]];
     kw.req_key[i] = id;
     atomicAdd(&kw.key_count[id * PV_CNT_PAD], 1u);
 }
 
-// Sort 2/3: exclusive prefix sum of key_count into key_cursor (one workgroup; nkeys <= kcap).
+// Exclusive prefix sum of one value per thread over a 1024-thread workgroup; *total = the sum.
+__device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
+    const uint32_t t = threadIdx.x;
+    __syncthreads();  // every thread is done with the previous scan's results
+    part[t] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    *total = part[1023];
+    return t ? part[t - 1] : 0u;
+}
+
+// Sort 2/3 (one workgroup): split the keys between the paths and give each key its slot range.
+// Comb keys (>= min_req requests, the first kcap of them in id order) take slots [0, CS) in id
+// order, every other key's requests the slots [CS, n). Threads own contiguous id ranges; three
+// passes over key_count: comb index, slot totals, cursors.
 __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
     __shared__ uint32_t part[1024];
-    const uint32_t nk = *kw.nkeys;
-    if (nk > kw.kcap) return;
+    const uint32_t nk = kw.nkeys[PV_SPLIT_KEYS];
     const uint32_t t = threadIdx.x;
     const uint32_t per = (nk + 1023) / 1024;
-    uint32_t sum = 0;
-    for (uint32_t j = 0; j < per; j++) {
-        const uint32_t id = t * per + j;
-        if (id < nk) sum += kw.key_count[id * PV_CNT_PAD];
+    const uint32_t lo = min(t * per, nk), hi = min(lo + per, nk);
+    uint32_t cand = 0;
+    for (uint32_t id = lo; id < hi; id++) cand += kw.key_count[id * PV_CNT_PAD] >= kw.min_req ? 1u : 0u;
+    uint32_t ncand;
+    const uint32_t jbase = pv_block_scan(cand, part, &ncand);
+    uint32_t cs = 0, ss = 0;
+    for (uint32_t id = lo, j = jbase; id < hi; id++) {
+        const uint32_t c = kw.key_count[id * PV_CNT_PAD];
+        if (c >= kw.min_req && j++ < kw.kcap) cs += c;
+        else ss += c;
     }
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the partials
-        const uint32_t v = t >= d ? part[t - d] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint32_t base = t ? part[t - 1] : 0u;
-    for (uint32_t j = 0; j < per; j++) {
-        const uint32_t id = t * per + j;
-        if (id < nk) {
-            kw.key_cursor[id * PV_CNT_PAD] = base;
-            base += kw.key_count[id * PV_CNT_PAD];
+    uint32_t ctotal, stotal;
+    uint32_t cc = pv_block_scan(cs, part, &ctotal);
+    uint32_t sc = ctotal + pv_block_scan(ss, part, &stotal);
+    for (uint32_t id = lo, j = jbase; id < hi; id++) {
+        const uint32_t c = kw.key_count[id * PV_CNT_PAD];
+        if (c >= kw.min_req && j < kw.kcap) {
+            kw.key_cid[id] = j;
+            kw.comb_key[j] = id;
+            kw.key_cursor[id * PV_CNT_PAD] = cc;
+            cc += c;
+        } else {
+            kw.key_cid[id] = PV_EMPTY;
+            kw.key_cursor[id * PV_CNT_PAD] = sc;
+            sc += c;
         }
+        if (c >= kw.min_req) j++;
+    }
+    if (t == 0) {
+        kw.nkeys[PV_SPLIT_COMB_KEYS] = min(ncand, kw.kcap);
+        kw.nkeys[PV_SPLIT_SLOTS] = ctotal;
     }
 }
 
 // Sort 3/3: each request takes the next slot of its key (order within a key is arbitrary).
-__global__ __launch_bounds__(PV_BLOCK) void pv_key_scatter_kernel(uint64_t n, KeyWork kw, Gate gate) {
-    if (!gate.comb()) return;
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_scatter_kernel(uint64_t n, KeyWork kw) {
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t id = kw.req_key[i];
     const uint32_t pos = atomicAdd(&kw.key_cursor[id * PV_CNT_PAD], 1u);
     kw.slot_req[pos] = i;
     kw.req_pos[i] = pos;
-    kw.skey[pos] = id;
+    kw.skey[pos] = kw.key_cid[id];
 }
 
 // Slot verdict bits back to request order: one ballot per 64 requests.
 __global__ __launch_bounds__(PV_BLOCK) void pv_unpermute_kernel(uint64_t n, KeyWork kw, uint64_t* __restrict__ verdict,
                                                                  Gate gate) {
-    if (!gate.comb()) return;
+    if (!gate.keyed()) return;
     const uint32_t r = blockIdx.x * PV_BLOCK + threadIdx.x;
     bool ok = false;
     if (r < n) {
@@ -578,12 +630,12 @@ struct DevBStage {  // fixed-base comb rows, entries of PV_BCOMB_STRIDE words (8
 // Per distinct key: libsodium's key checks, -A, and the chain of bases [256^i](-A).
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
                                                                     Gate gate) {
-    if (!gate.comb()) return;
+    if (!gate.keyed()) return;
     __builtin_amdgcn_s_setprio(3);
-    const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;
-    if (id >= *kw.nkeys) return;
+    const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;  // comb index
+    if (id >= kw.nkeys[PV_SPLIT_COMB_KEYS]) return;
     uint32_t A[8];
-    pv_load_pk(A, pk, kw.key_owner[id]);
+    pv_load_pk(A, pk, kw.key_owner[kw.comb_key[id]]);
     ge_p3 negA;
     const bool ok = pv_key_ok_negate(negA, A);
     kw.key_flag[id] = ok ? 1u : 0u;
@@ -655,20 +707,20 @@ __device__ __forceinline__ void pv_quad_dbl(fe& X, fe& Y, fe& Z, fe& T, const Qu
 // Per distinct key, four lanes: libsodium's key checks, -A, and the bases [256^i](-A), i = 0..31.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
                                                                          Gate gate) {
-    if (!gate.comb()) return;
+    if (!gate.keyed()) return;
     // the chain is the batch's critical path and shares SIMDs with the per-request prep kernel:
     // take issue priority over it
     __builtin_amdgcn_s_setprio(3);
     const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
-    const uint32_t nk = *kw.nkeys;
-    const uint32_t id = g >> 2;
+    const uint32_t nk = kw.nkeys[PV_SPLIT_COMB_KEYS];
+    const uint32_t id = g >> 2;  // comb index
     uint32_t rl = g & 3;
     asm volatile("" : "+v"(rl));  // opaque: keep the per-role selects branch-free
     const QuadRole role{rl == 0 ? ~0u : 0u, rl == 1 ? ~0u : 0u, rl == 2 ? ~0u : 0u};
     // whole quads exit together (nk is uniform), so the DPP partners of a live lane are live
     if (id >= nk) return;
     uint32_t A[8];
-    pv_load_pk(A, pk, kw.key_owner[id]);
+    pv_load_pk(A, pk, kw.key_owner[kw.comb_key[id]]);
     ge_p3 cur;
     const bool ok = pv_key_ok_negate(cur, A);
     if (rl == 0) kw.key_flag[id] = ok ? 1u : 0u;
@@ -694,8 +746,8 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const ui
 
 // Per (key, position, block of 16 entries): the comb table rows. Grid-stride over nkeys * 256 items.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_fill_kernel(KeyWork kw, Gate gate) {
-    if (!gate.comb()) return;
-    const uint32_t items = *kw.nkeys * PV_COMB_POS * PV_COMB_BLOCKS;
+    if (!gate.keyed()) return;
+    const uint32_t items = kw.nkeys[PV_SPLIT_COMB_KEYS] * PV_COMB_POS * PV_COMB_BLOCKS;
     for (uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x; it < items; it += gridDim.x * PV_BLOCK) {
         const uint32_t id = it / (PV_COMB_POS * PV_COMB_BLOCKS);
         const int pos = (it / PV_COMB_BLOCKS) % PV_COMB_POS;
@@ -710,9 +762,9 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
                                                                     const uint64_t* __restrict__ off, uint64_t n,
                                                                     const uint8_t* __restrict__ pk, Work wk,
                                                                     KeyWork kw, Gate gate) {
-    if (!gate.comb()) return;
+    if (!gate.keyed()) return;
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
-    if (i >= n) return;
+    if (i >= gate.ncomb()) return;
     const uint32_t r = kw.slot_req[i];                         // request
     const uint64_t o0 = off[r], o1 = off[r + 1];
     const uint64_t smlen = o1 - o0;
@@ -747,9 +799,9 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
 // acc (extended, 40 words) goes to q rows 0..39.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
                                                                  Gate gate) {
-    if (!gate.comb()) return;
-    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
-    if (i >= n) return;
+    if (!gate.keyed()) return;
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
+    if (i >= gate.ncomb()) return;
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     ge_p3 acc;
 #if PV_COMB_PIPELINE
@@ -790,10 +842,10 @@ __device__ __forceinline__ uint32_t pv_xcd_block() {
 // Q to q rows 0..29; the key's own libsodium checks are folded into flags[i] here.
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                Gate gate) {
-    if (!gate.comb()) return;
+    if (!gate.keyed()) return;
     const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
-    if (i >= n) return;
-    const uint32_t id = kw.skey[i];
+    if (i >= gate.ncomb()) return;
+    const uint32_t id = kw.skey[i];  // comb index
     const uint32_t S = (uint32_t)wk.stride;
     const Soa qs(wk.q, 40, wk.stride);
     ge_p3 acc;
@@ -879,7 +931,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* _
                                                                  const uint64_t* __restrict__ off, uint64_t n,
                                                                  Work wk, uint64_t* __restrict__ verdict,
                                                                  KeyWork kw, Gate gate) {
-    const bool comb = gate.comb();
+    const bool comb = gate.keyed();  // slot order
     const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t w = g >> 6, l = g & 63;
     const DevEncSrc src{Soa(wk.q, 40, wk.stride), w, l, n};
@@ -904,10 +956,13 @@ struct Ctx {
     hipStream_t kstream = nullptr;           // per-key pipeline (chain + table fill), overlapped
     hipEvent_t ev_keys_ready = nullptr;      // dedup done (main -> kstream)
     hipEvent_t ev_tables_ready = nullptr;    // comb tables done (kstream -> main)
+    hipStream_t sstream = nullptr;           // Straus-path slots of a split chunk, overlapped
+    hipEvent_t ev_straus_done = nullptr;     // their q / flags written (sstream -> main)
     uint32_t* d_btab = nullptr;
     Work work{nullptr, nullptr, nullptr, nullptr, 0};
     KeyWork kw{};
-    uint32_t last_limit = 0;  // comb-path key limit of the most recent chunk (0: Straus forced)
+    bool last_keyed = false;  // the most recent chunk ran the dedup / split kernels
+    uint32_t last_split[3] = {0, 0, 0};  // PV_SPLIT_* of it, read back by pv_last_path
     uint4* d_bcomb = nullptr;  // fixed-base comb T_B
     int path = PV_PATH_AUTO;
     // host-entry staging
@@ -991,36 +1046,33 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
         };
         int rc = mark(PV_STAGE_KEYS);
         if (rc) return rc;
-        // Path choice (measured round-1 costs on MI355X): the comb path pays ~0.3 ms of fixed
-        // work per chunk (dedup, sort, chain latency) and ~0.47 us per distinct key (its 4,128-entry
-        // table), then ~3 ns per request against ~13 ns on the Straus path. AUTO therefore takes it
-        // when distinct keys <= (10 ns x n - 0.3 ms) / 0.47 us ~= 0.021 n - 640; the decision is
-        // made on the device from the dedup count (Gate), so nothing synchronises.
-        uint32_t limit = 0;
-        if (g_ctx.path == PV_PATH_COMB) {
-            limit = g_ctx.kw.kcap;
-        } else if (g_ctx.path == PV_PATH_AUTO) {
-            const int64_t l = ((int64_t)m * 21 - 640000) / 1000;
-            limit = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(g_ctx.kw.kcap, l));
-        }
-        Gate gate{nullptr, 0};
-        g_ctx.last_limit = limit;
-        if (limit > 0) {
-            KeyWork& kw = g_ctx.kw;
+        // Path split (measured round-1 costs on MI355X): a key's comb table costs ~0.47 us of device
+        // time (chain + 4,128-entry fill) and then saves ~10 ns per request against the Straus
+        // path (~3 vs ~13 ns), so AUTO gives a table to keys with >= PV_COMB_MIN_REQ requests in
+        // the chunk and verifies every other request on the Straus path in the same launch. The
+        // split is computed on the device by the dedup/sort kernels (Gate); nothing synchronises.
+        // Chunks below PV_KEYED_MIN requests skip dedup (~0.3 ms of fixed work) and go Straus.
+        const bool keyed = g_ctx.path == PV_PATH_COMB || (g_ctx.path == PV_PATH_AUTO && m >= PV_KEYED_MIN);
+        Gate gate{nullptr, nullptr};
+        g_ctx.last_keyed = keyed;
+        KeyWork kw = g_ctx.kw;
+        kw.min_req = g_ctx.path == PV_PATH_COMB ? 1u : (uint32_t)PV_COMB_MIN_REQ;
+        const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
+        if (keyed) {
             PV_HIP(hipMemsetAsync(kw.slot, 0xFF, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
-            PV_HIP(hipMemsetAsync(kw.nkeys, 0, 4, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipMemsetAsync(kw.nkeys, 0, 16, stream), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            gate = Gate{kw.nkeys, limit};
-            // key-sorted slot order for the per-request comb kernels
-            PV_HIP(hipMemsetAsync(kw.key_count, 0, (uint64_t)kw.kcap * PV_CNT_PAD * 4, stream), PV_ERR_LAUNCH);
+            gate = Gate{kw.nkeys, kw.slot_req};
+            // key-sorted slot order: comb keys' requests first, then the Straus requests
+            PV_HIP(hipMemsetAsync(kw.key_count, 0, m * PV_CNT_PAD * 4, stream), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_count_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(1024), 0, stream, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_key_scatter_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw, gate);
+            hipLaunchKernelGGL(pv_key_scatter_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             // the per-key chain (few, long-latency lanes) and the table fill run on kstream,
             // overlapped with the per-request prep on the main stream
@@ -1036,26 +1088,30 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             const uint64_t items = (uint64_t)limit * PV_COMB_POS * PV_COMB_BLOCKS;
             const unsigned fgrid = (unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096);
-            hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, g_ctx.kstream, g_ctx.kw, gate);
+            hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, g_ctx.kstream, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.kstream), PV_ERR_LAUNCH);
         }
         if ((rc = mark(PV_STAGE_PREP))) return rc;
-        hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                           d_pk + 32 * c0, g_ctx.work, gate);
-        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (limit > 0) {
-            // The Straus kernels go first: when the gate picks the comb path they exit at their first
-            // instruction, and here, with only the few key-chain waves resident, their 4,096
-            // workgroups drain in microseconds. Launched between the comb kernels instead, the gated
-            // table kernel waited ~170 us for CUs held by the table fill (round-1 trace).
-            hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
+        if (keyed) {
+            // The Straus-path slots of a split chunk (keys without a table: usually a few
+            // thousand one-off requests) run on their own stream beside the comb kernels: their
+            // waves take ~1 ms from start to end however few they are, which on the main stream
+            // would delay the whole comb path. Their blocks are dispatched from the END of the slot
+            // range (where the Straus slots are), and blocks of comb slots exit at once.
+            hipStream_t ss = g_ctx.sstream;
+            PV_HIP(hipStreamWaitEvent(ss, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
+                               d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+            hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                g_ctx.d_btab, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            PV_HIP(hipEventRecord(g_ctx.ev_straus_done, ss), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                               d_pk + 32 * c0, g_ctx.work, g_ctx.kw, gate);
+                               d_pk + 32 * c0, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             // [S]B while the key stream finishes the tables, then join
@@ -1064,9 +1120,13 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
-            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.kw, gate);
+            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_straus_done, 0), PV_ERR_LAUNCH);
         } else {
+            hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+                               d_pk + 32 * c0, g_ctx.work, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -1078,10 +1138,10 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
         if ((rc = mark(PV_STAGE_ENCODE))) return rc;
         const unsigned egrid = (unsigned)((m + PV_BLOCK * PV_ENC_BATCH - 1) / (PV_BLOCK * PV_ENC_BATCH));
         hipLaunchKernelGGL(pv_encode_kernel, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                           g_ctx.work, d_verdict + c0 / 64, g_ctx.kw, gate);
+                           g_ctx.work, d_verdict + c0 / 64, kw, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        if (limit > 0) {
-            hipLaunchKernelGGL(pv_unpermute_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.kw,
+        if (keyed) {
+            hipLaunchKernelGGL(pv_unpermute_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw,
                                d_verdict + c0 / 64, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         }
@@ -1125,6 +1185,8 @@ int pv_init(int device) {
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.kstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_keys_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     std::vector<uint32_t> bt(PV_BTAB_ENTRIES * PV_BTAB_STRIDE);
     pv_build_b_table(bt.data());
     PV_HIP(hipMalloc((void**)&g_ctx.d_btab, bt.size() * 4), PV_ERR_ALLOC);
@@ -1145,12 +1207,14 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.slot_id, H * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_key, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.nkeys, 256), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_owner, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_owner, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_cid, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.comb_key, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_PTS * 160), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_count, (uint64_t)kw.kcap * PV_CNT_PAD * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_cursor, (uint64_t)kw.kcap * PV_CNT_PAD * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_count, S * PV_CNT_PAD * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_cursor, S * PV_CNT_PAD * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.slot_req, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_pos, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.skey, S * 4), PV_ERR_ALLOC);
@@ -1184,7 +1248,8 @@ void pv_shutdown(void) {
     if (g_ctx.work.flags) (void)hipFree(g_ctx.work.flags);
     if (g_ctx.work.q) (void)hipFree(g_ctx.work.q);
     for (void* p : {(void*)g_ctx.kw.slot, (void*)g_ctx.kw.slot_id, (void*)g_ctx.kw.req_key, (void*)g_ctx.kw.nkeys,
-                    (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
+                    (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_cid, (void*)g_ctx.kw.comb_key,
+                    (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
                     (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb, (void*)g_ctx.kw.key_count,
                     (void*)g_ctx.kw.key_cursor, (void*)g_ctx.kw.slot_req, (void*)g_ctx.kw.req_pos,
                     (void*)g_ctx.kw.skey, (void*)g_ctx.kw.sverdict})
@@ -1194,19 +1259,32 @@ void pv_shutdown(void) {
     if (g_ctx.kstream) (void)hipStreamDestroy(g_ctx.kstream);
     if (g_ctx.ev_keys_ready) (void)hipEventDestroy(g_ctx.ev_keys_ready);
     if (g_ctx.ev_tables_ready) (void)hipEventDestroy(g_ctx.ev_tables_ready);
+    if (g_ctx.sstream) (void)hipStreamDestroy(g_ctx.sstream);
+    if (g_ctx.ev_straus_done) (void)hipEventDestroy(g_ctx.ev_straus_done);
     g_ctx = Ctx();
 }
 
 int pv_last_path(int* path, uint32_t* nkeys) {
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_last_path: call pv_init first");
-    uint32_t u = 0;
-    if (g_ctx.last_limit > 0) {
+    uint32_t u[4] = {0, 0, 0, 0};
+    if (g_ctx.last_keyed) {
         PV_HIP(hipStreamSynchronize(g_ctx.stream), PV_ERR_LAUNCH);
         PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
-        PV_HIP(hipMemcpy(&u, g_ctx.kw.nkeys, 4, hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpy(u, g_ctx.kw.nkeys, 12, hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
     }
-    if (nkeys) *nkeys = u;
-    if (path) *path = (g_ctx.last_limit > 0 && u <= g_ctx.last_limit) ? PV_PATH_COMB : PV_PATH_STRAUS;
+    if (nkeys) *nkeys = u[PV_SPLIT_KEYS];
+    if (path) *path = u[PV_SPLIT_SLOTS] > 0 ? PV_PATH_COMB : PV_PATH_STRAUS;
+    g_ctx.last_split[0] = u[PV_SPLIT_KEYS];
+    g_ctx.last_split[1] = u[PV_SPLIT_COMB_KEYS];
+    g_ctx.last_split[2] = u[PV_SPLIT_SLOTS];
+    return PV_OK;
+}
+
+int pv_last_split(uint32_t* keys, uint32_t* comb_keys, uint32_t* comb_requests) {
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_last_split: call pv_init first");
+    if (keys) *keys = g_ctx.last_split[0];
+    if (comb_keys) *comb_keys = g_ctx.last_split[1];
+    if (comb_requests) *comb_requests = g_ctx.last_split[2];
     return PV_OK;
 }
 

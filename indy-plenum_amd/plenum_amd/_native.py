@@ -37,6 +37,7 @@ SIGNATURES = {
     "pv_set_timing": (ctypes.c_int, [ctypes.c_int]),
     "pv_set_path": (ctypes.c_int, [ctypes.c_int]),
     "pv_last_path": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32)]),
+    "pv_last_split": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)] * 3),
     "pv_stage_times": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "pv_kernel_times": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
@@ -160,6 +161,15 @@ def last_path():
     p, u = ctypes.c_int(), ctypes.c_uint32()
     check(lib().pv_last_path(ctypes.byref(p), ctypes.byref(u)), "pv_last_path")
     return p.value, u.value
+
+
+def last_split():
+    """(distinct keys, keys with a comb table, requests verified with them) of the most recent
+    chunk; the remaining requests took the Straus path. Synchronises (via pv_last_path)."""
+    last_path()
+    v = [ctypes.c_uint32() for _ in range(3)]
+    check(lib().pv_last_split(*[ctypes.byref(x) for x in v]), "pv_last_split")
+    return tuple(x.value for x in v)
 
 
 def _blob(items):

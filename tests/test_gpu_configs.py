@@ -42,11 +42,18 @@ def test_config3_1M_adversarial_bit_exact(native, nym1m, oracle):
     want = cpu_verdicts(blob2, off, pks2)
     # both arithmetic paths: the per-request Straus path and the keyed comb path (~10k distinct
     # keys here: the 1,024 signers plus every mutated key)
-    for path in (native.PV_PATH_STRAUS, native.PV_PATH_COMB):
+    for path in (native.PV_PATH_STRAUS, native.PV_PATH_COMB, native.PV_PATH_AUTO):
         native.set_path(path)
         got = native.verify_sm_batch(blob2, off, pks2)
+        split = native.last_split()
         native.set_path(native.PV_PATH_AUTO)
         assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
+        if path == native.PV_PATH_AUTO:
+            # the 1,024 signers get comb tables; the adversarial one-request keys take the Straus
+            # path in the same launch
+            # (plus the few adversarial keys that recur: blacklisted / non-canonical encodings)
+            assert 1024 <= split[1] < 1200 and split[0] > split[1], split
+            assert len(got) - 30000 < split[2] < len(got), split
     # the untouched 98 % are valid and the mutated records are (almost all) rejected
     mask = np.ones(len(got), bool)
     mask[idx] = False
@@ -197,4 +204,64 @@ def test_config5_shard_8M(native, nym1m):
     want[bad] = False
     got = native.verify_sm_batch(blob8, off8, pks8)
     assert len(got) == n
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
+def _split_batch(sodium, n_signed, n_single, seed):
+    """n_signed NYM requests from the 1,024-signer pool (n_signed / 1,024 per key) plus n_single
+    requests that each carry their own key, shuffled, with ~1 % of records corrupted."""
+    import nym_workload
+    rng = np.random.default_rng(seed)
+    recs, keys = [], []
+    if n_signed:
+        blob, off, pks = nym_workload.generate(7000, n_signed, workers=8)
+        recs = [blob[off[i]:off[i + 1]].tobytes() for i in range(n_signed)]
+        keys = [pks[i].tobytes() for i in range(n_signed)]
+    for j in range(n_single):
+        pk, sk = sodium.seed_keypair(rng.bytes(32))
+        m = rng.bytes(int(rng.integers(0, 320)))
+        recs.append(sodium.sign_detached(m, sk) + m)
+        keys.append(pk)
+    perm = rng.permutation(len(recs))
+    recs = [bytearray(recs[i]) for i in perm]
+    keys = [keys[i] for i in perm]
+    bad = rng.choice(len(recs), len(recs) // 100, replace=False)
+    for i in bad:
+        recs[i][int(rng.integers(0, 64))] ^= 1 << int(rng.integers(0, 8))
+    off2 = np.zeros(len(recs) + 1, np.uint64)
+    np.cumsum([len(r) for r in recs], out=off2[1:])
+    return (np.frombuffer(b"".join(bytes(r) for r in recs), np.uint8), off2,
+            np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 32))
+
+
+def test_split_paths_in_one_launch(native, sodium):
+    """Frequent signers and one-off keys in one chunk: AUTO gives tables to the 1,024 frequent keys
+    (60 requests each) and verifies the 20,000 one-off requests on the Straus path; forced COMB
+    gives tables to the first 16,384 keys only (the capacity) and the rest go Straus; every path
+    bit-exact against libsodium."""
+    from oracle.oracle import cpu_verdicts
+    blob, off, pks = _split_batch(sodium, 61440, 20000, seed=11)
+    n = len(off) - 1
+    want = cpu_verdicts(blob, off, pks)
+    assert 0 < (~want).sum() < n // 50
+    for path in (native.PV_PATH_AUTO, native.PV_PATH_COMB, native.PV_PATH_STRAUS):
+        native.set_path(path)
+        got = native.verify_sm_batch(blob, off, pks)
+        split = native.last_split()
+        native.set_path(native.PV_PATH_AUTO)
+        assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
+        if path == native.PV_PATH_AUTO:
+            assert split == (21024, 1024, 61440), split
+        elif path == native.PV_PATH_COMB:
+            assert split[0] == 21024 and split[1] == 16384 and 16384 < split[2] < n, split
+
+
+def test_split_all_keys_distinct(native, sodium):
+    """A chunk big enough for dedup in which no key repeats: AUTO builds no table and every request
+    goes through the Straus path in slot order."""
+    from oracle.oracle import cpu_verdicts
+    blob, off, pks = _split_batch(sodium, 0, 40000, seed=12)
+    want = cpu_verdicts(blob, off, pks)
+    got = native.verify_sm_batch(blob, off, pks)
+    assert native.last_split() == (40000, 0, 0)
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
