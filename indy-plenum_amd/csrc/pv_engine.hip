@@ -180,9 +180,11 @@ struct Gate {
     const uint32_t* split;
     const uint32_t* slot_req;
     __device__ __forceinline__ bool keyed() const { return split != nullptr; }
-    // block of a Straus-path kernel: from the end of the slot range when split (the Straus slots
-    // are the last ones, so the blocks with work are dispatched first)
-    __device__ __forceinline__ uint32_t sblock() const { return split ? gridDim.x - 1 - blockIdx.x : blockIdx.x; }
+    // Straus-path kernels loop over 256-slot tiles t = blockIdx.x, blockIdx.x + gridDim.x, ...;
+    // split, the tiles are taken from the END of the slot range (where the Straus slots are) and a
+    // small grid strides over them, so the first tile with no Straus slot ends the loop and no
+    // flood of empty workgroups competes with the comb kernels for CUs.
+    __device__ __forceinline__ uint32_t stile(uint32_t t, uint32_t ntiles) const { return split ? ntiles - 1 - t : t; }
     __device__ __forceinline__ uint32_t ncomb() const { return split ? split[PV_SPLIT_SLOTS] : 0u; }
     // request of a Straus-path slot
     __device__ __forceinline__ uint32_t req(uint32_t i) const { return split ? slot_req[i] : i; }
@@ -191,8 +193,8 @@ struct Gate {
 // Keyed workspace (comb.h). The hash table maps a 32-byte key to the index of the first request
 // that carried it; slot_id gives the dense key id of an owned slot (ids < chunk size).
 //   slot     [H] u32   owner request index, PV_EMPTY = free
-//   slot_id  [H] u32   dense key id of an owned slot
-//   req_key  [stride]  the request's slot, then (after pv_key_count) its key id
+//   slot_id  [H] u32   dense key id of an owned slot;  slot_cnt [H] requests carrying its key
+//   req_key  [stride]  the request's hash slot;         req_rank [stride] its rank among them
 //   nkeys    [3]       PV_SPLIT_* counters (see Gate)
 //   key_owner[stride]  a request carrying key id
 //   key_cid  [stride]  comb index of key id (PV_EMPTY: its requests take the Straus path)
@@ -206,13 +208,15 @@ struct Gate {
 // Key-sorted processing order ("slots"): after dedup the requests of each key occupy a contiguous
 // range of slots, comb keys first, so consecutive lanes and waves read the same key's table rows
 // (L2-resident) instead of 1,024 keys' tables at random:
-//   key_count[stride], key_cursor[stride]  requests per key, then the next free slot of each key
+//   key_count[stride], key_cursor[stride]  requests per key id, then the key's first slot
 //   slot_req [stride]                   slot -> request index;  req_pos [stride] request -> slot
 //   skey     [stride]                   slot -> comb index;     sverdict [stride / 64] slot verdicts
 struct KeyWork {
     uint32_t* slot;
     uint32_t* slot_id;
+    uint32_t* slot_cnt;
     uint32_t* req_key;
+    uint32_t* req_rank;
     uint32_t* nkeys;
     uint32_t* key_owner;
     uint32_t* key_cid;
@@ -232,22 +236,14 @@ struct KeyWork {
     uint32_t min_req;
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
-// key_count / key_cursor hold one counter per 64 B: every request bumps its key's counter, and with
-// 1,024 keys packed 32 to a cache line the atomics of a 1M-request chunk queued on 32 lines of L2
-static constexpr uint32_t PV_CNT_PAD = 16;
 #ifndef PV_COMB_MIN_REQ
 #define PV_COMB_MIN_REQ 48
 #endif
 
-// Kernel 1: checks, decompression of A, k = SHA-512(R||A||M) mod L, table of [j](-A), recoding.
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __restrict__ sm,
-                                                               const uint64_t* __restrict__ off, uint64_t n,
-                                                               const uint8_t* __restrict__ pk, Work wk, Gate gate) {
-    const uint32_t nc = gate.ncomb(), sb = gate.sblock();
-    if ((sb + 1) * PV_BLOCK <= nc) return;  // a block of comb-path slots
-    const uint64_t i = (uint64_t)sb * PV_BLOCK + threadIdx.x;  // slot
-    if (i >= n || i < nc) return;
-    const uint32_t r = gate.req((uint32_t)i);                          // request
+// Straus path, per slot i (request r): checks, decompression of A, k = SHA-512(R||A||M) mod L,
+// recoding; -A for the table kernel.
+__device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, const uint64_t* __restrict__ off,
+                                             const uint8_t* __restrict__ pk, const Work& wk, uint32_t i, uint32_t r) {
     const uint64_t o0 = off[r], o1 = off[r + 1];
     const uint64_t smlen = o1 - o0;
     const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
@@ -289,24 +285,40 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __r
     wk.flags[i] = ok ? 1u : 0u;
 }
 
+// Kernel 1 (Straus path): pv_prep_slot over the Straus slots.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __restrict__ sm,
+                                                               const uint64_t* __restrict__ off, uint64_t n,
+                                                               const uint8_t* __restrict__ pk, Work wk, Gate gate) {
+    const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t sb = gate.stile(t, ntiles);
+        if ((sb + 1) * PV_BLOCK <= nc) break;  // this and every later tile: comb-path slots
+        const uint32_t i = sb * PV_BLOCK + threadIdx.x;  // slot
+        if (i < n && i >= nc) pv_prep_slot(sm, off, pk, wk, i, gate.req(i));
+    }
+}
+
 // Kernel 1b: expand -A (extended, in slot 1) into the cached table [j](-A), j = 0..8.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk, Gate gate) {
-    const uint32_t nc = gate.ncomb(), sb = gate.sblock();
-    if ((sb + 1) * PV_BLOCK <= nc) return;
-    const uint64_t i = (uint64_t)sb * PV_BLOCK + threadIdx.x;  // slot
-    if (i >= n || i < nc) return;
-    const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
-    uint32_t w[40];
-    at.load(1, w);
-    ge_p3 negA;
+    const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t sb = gate.stile(t, ntiles);
+        if ((sb + 1) * PV_BLOCK <= nc) break;
+        const uint32_t i = sb * PV_BLOCK + threadIdx.x;  // slot
+        if (i >= n || i < nc) continue;
+        const DevATab at{wk.atab, (uint32_t)wk.stride, i};
+        uint32_t w[40];
+        at.load(1, w);
+        ge_p3 negA;
 #pragma unroll
-    for (int q = 0; q < 10; q++) {
-        negA.X.v[q] = w[q];
-        negA.Y.v[q] = w[10 + q];
-        negA.Z.v[q] = w[20 + q];
-        negA.T.v[q] = w[30 + q];
+        for (int q = 0; q < 10; q++) {
+            negA.X.v[q] = w[q];
+            negA.Y.v[q] = w[10 + q];
+            negA.Z.v[q] = w[20 + q];
+            negA.T.v[q] = w[30 + q];
+        }
+        pv_build_a_table(at, negA);
     }
-    pv_build_a_table(at, negA);
 }
 
 // Kernel 2: Q = [S]B + [k](-A) by the regular-window Straus loop, encode, compare with R, ballot.
@@ -314,27 +326,31 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
                                                               const uint64_t* __restrict__ off, uint64_t n,
                                                               const uint32_t* __restrict__ btab_g, Work wk,
                                                               Gate gate) {
-    const uint32_t nc = gate.ncomb(), sb = gate.sblock();
-    if ((sb + 1) * PV_BLOCK <= nc) return;  // a block of comb-path slots (before the LDS fill)
+    const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
+    if (blockIdx.x >= ntiles || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;  // before the LDS fill
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
     for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
         reinterpret_cast<uint4*>(sbt)[t] = reinterpret_cast<const uint4*>(btab_g)[t];
     __syncthreads();
-    const uint64_t i0 = (uint64_t)sb * PV_BLOCK + threadIdx.x;  // slot
-    const bool active = i0 < n && i0 >= nc;
-    const uint64_t i = active ? i0 : n - 1;  // n - 1 >= nc here: a Straus slot
-    const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
     const LdsBTab bt{sbt};
-    const DevDigits dig{wk.digits, (uint32_t)wk.stride, (uint32_t)i};
-    fe X, Y, Z;
-    pv_straus_xyz(X, Y, Z, at, bt, dig);
-    if (active) {
-        const Soa qs(wk.q, 40, wk.stride);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t sb = gate.stile(t, ntiles);
+        if ((sb + 1) * PV_BLOCK <= nc) break;
+        const uint32_t i0 = sb * PV_BLOCK + threadIdx.x;  // slot
+        const bool active = i0 < n && i0 >= nc;
+        const uint32_t i = active ? i0 : (uint32_t)n - 1;  // n - 1 >= nc here: a Straus slot
+        const DevATab at{wk.atab, (uint32_t)wk.stride, i};
+        const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
+        fe X, Y, Z;
+        pv_straus_xyz(X, Y, Z, at, bt, dig);
+        if (active) {
+            const Soa qs(wk.q, 40, wk.stride);
 #pragma unroll
-        for (int q = 0; q < 10; q++) {
-            qs.st(q, (uint32_t)i, X.v[q]);
-            qs.st(10 + q, (uint32_t)i, Y.v[q]);
-            qs.st(20 + q, (uint32_t)i, Z.v[q]);
+            for (int q = 0; q < 10; q++) {
+                qs.st(q, i, X.v[q]);
+                qs.st(10 + q, i, Y.v[q]);
+                qs.st(20 + q, i, Z.v[q]);
+            }
         }
     }
 }
@@ -378,26 +394,29 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* 
         h = (h + 1) & kw.hmask;
     }
     kw.req_key[i] = h;
+    // the request's rank among its key's requests, and (final after this kernel) the key's count;
+    // the 1,024-odd counters of a batch sit on distinct hash slots, i.e. mostly distinct L2 lines
+    kw.req_rank[i] = atomicAdd(&kw.slot_cnt[h], 1u);
 }
 
-// Dedup 2/2: the owner request of each occupied slot takes a dense key id.
+// Dedup 2/2: the owner request of each occupied slot takes a dense key id (one atomic per wave)
+// and records its key's request count.
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, KeyWork kw) {
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t s = kw.req_key[i];
-    if (kw.slot[s] != i) return;
-    const uint32_t id = atomicAdd(&kw.nkeys[PV_SPLIT_KEYS], 1u);  // < n
+    const uint32_t s = i < n ? kw.req_key[i] : 0u;
+    const bool own = i < n && kw.slot[s] == i;
+    const uint64_t owners = __ballot(own);
+    if (owners == 0) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)owners) - 1u;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&kw.nkeys[PV_SPLIT_KEYS], (uint32_t)__popcll(owners));
+    base = __shfl(base, (int)leader);
+    if (!own) return;
+    const uint32_t id = base + (uint32_t)__popcll(owners & ((1ull << lane) - 1ull));  // < n
     kw.slot_id[s] = id;
     kw.key_owner[id] = i;
-}
-
-// Sort 1/3: dense key id per request (req_key: slot -> id) and requests per key.
-__global__ __launch_bounds__(PV_BLOCK) void pv_key_count_kernel(uint64_t n, KeyWork kw) {
-    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t id = kw.slot_id[kw.req_key[i]];
-    kw.req_key[i] = id;
-    atomicAdd(&kw.key_count[id * PV_CNT_PAD], 1u);
+    kw.key_count[id] = kw.slot_cnt[s];
 }
 
 // Exclusive prefix sum of one value per thread over a 1024-thread workgroup; *total = the sum.
@@ -427,12 +446,12 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
     const uint32_t per = (nk + 1023) / 1024;
     const uint32_t lo = min(t * per, nk), hi = min(lo + per, nk);
     uint32_t cand = 0;
-    for (uint32_t id = lo; id < hi; id++) cand += kw.key_count[id * PV_CNT_PAD] >= kw.min_req ? 1u : 0u;
+    for (uint32_t id = lo; id < hi; id++) cand += kw.key_count[id] >= kw.min_req ? 1u : 0u;
     uint32_t ncand;
     const uint32_t jbase = pv_block_scan(cand, part, &ncand);
     uint32_t cs = 0, ss = 0;
     for (uint32_t id = lo, j = jbase; id < hi; id++) {
-        const uint32_t c = kw.key_count[id * PV_CNT_PAD];
+        const uint32_t c = kw.key_count[id];
         if (c >= kw.min_req && j++ < kw.kcap) cs += c;
         else ss += c;
     }
@@ -440,15 +459,15 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
     uint32_t cc = pv_block_scan(cs, part, &ctotal);
     uint32_t sc = ctotal + pv_block_scan(ss, part, &stotal);
     for (uint32_t id = lo, j = jbase; id < hi; id++) {
-        const uint32_t c = kw.key_count[id * PV_CNT_PAD];
+        const uint32_t c = kw.key_count[id];
         if (c >= kw.min_req && j < kw.kcap) {
             kw.key_cid[id] = j;
             kw.comb_key[j] = id;
-            kw.key_cursor[id * PV_CNT_PAD] = cc;
+            kw.key_cursor[id] = cc;
             cc += c;
         } else {
             kw.key_cid[id] = PV_EMPTY;
-            kw.key_cursor[id * PV_CNT_PAD] = sc;
+            kw.key_cursor[id] = sc;
             sc += c;
         }
         if (c >= kw.min_req) j++;
@@ -459,12 +478,12 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
     }
 }
 
-// Sort 3/3: each request takes the next slot of its key (order within a key is arbitrary).
+// Sort 3/3: each request takes its key's first slot + its rank among the key's requests.
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_scatter_kernel(uint64_t n, KeyWork kw) {
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
     if (i >= n) return;
-    const uint32_t id = kw.req_key[i];
-    const uint32_t pos = atomicAdd(&kw.key_cursor[id * PV_CNT_PAD], 1u);
+    const uint32_t id = kw.slot_id[kw.req_key[i]];
+    const uint32_t pos = kw.key_cursor[id] + kw.req_rank[i];
     kw.slot_req[pos] = i;
     kw.req_pos[i] = pos;
     kw.skey[pos] = kw.key_cid[id];
@@ -1060,6 +1079,7 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
         const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
         if (keyed) {
             PV_HIP(hipMemsetAsync(kw.slot, 0xFF, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipMemsetAsync(kw.slot_cnt, 0, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
             PV_HIP(hipMemsetAsync(kw.nkeys, 0, 16, stream), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -1067,9 +1087,6 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             gate = Gate{kw.nkeys, kw.slot_req};
             // key-sorted slot order: comb keys' requests first, then the Straus requests
-            PV_HIP(hipMemsetAsync(kw.key_count, 0, m * PV_CNT_PAD * 4, stream), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_key_count_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
-            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(1024), 0, stream, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_scatter_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
@@ -1100,13 +1117,14 @@ int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t
             // would delay the whole comb path. Their blocks are dispatched from the END of the slot
             // range (where the Straus slots are), and blocks of comb slots exit at once.
             hipStream_t ss = g_ctx.sstream;
+            const unsigned sgrid = std::min<unsigned>(grid, 2u * (unsigned)std::max(1, g_ctx.cus));
             PV_HIP(hipStreamWaitEvent(ss, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
+            hipLaunchKernelGGL(pv_prep_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, gate);
+            hipLaunchKernelGGL(pv_table_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
+            hipLaunchKernelGGL(pv_msm_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                g_ctx.d_btab, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipEventRecord(g_ctx.ev_straus_done, ss), PV_ERR_LAUNCH);
@@ -1205,7 +1223,9 @@ int pv_init(int device) {
         kw.seed = (uint32_t)std::random_device{}() | 1u;
         PV_HIP(hipMalloc((void**)&kw.slot, H * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.slot_id, H * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.slot_cnt, H * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_key, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.req_rank, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.nkeys, 256), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_owner, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_cid, S * 4), PV_ERR_ALLOC);
@@ -1213,8 +1233,8 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_PTS * 160), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_count, S * PV_CNT_PAD * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_cursor, S * PV_CNT_PAD * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_count, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_cursor, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.slot_req, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_pos, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.skey, S * 4), PV_ERR_ALLOC);
@@ -1247,7 +1267,8 @@ void pv_shutdown(void) {
     if (g_ctx.work.digits) (void)hipFree(g_ctx.work.digits);
     if (g_ctx.work.flags) (void)hipFree(g_ctx.work.flags);
     if (g_ctx.work.q) (void)hipFree(g_ctx.work.q);
-    for (void* p : {(void*)g_ctx.kw.slot, (void*)g_ctx.kw.slot_id, (void*)g_ctx.kw.req_key, (void*)g_ctx.kw.nkeys,
+    for (void* p : {(void*)g_ctx.kw.slot, (void*)g_ctx.kw.slot_id, (void*)g_ctx.kw.slot_cnt, (void*)g_ctx.kw.req_key,
+                    (void*)g_ctx.kw.req_rank, (void*)g_ctx.kw.nkeys,
                     (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_cid, (void*)g_ctx.kw.comb_key,
                     (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
                     (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb, (void*)g_ctx.kw.key_count,
