@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build engine variants (compile-time switches) next to each other for A/B timing on the GPU:
 #   microbench/build_variants.sh NAME "-DFLAG=.. ..." [NAME "FLAGS" ...]  -> microbench/variants/NAME.so
-# Load one with PLENUM_AMD_LIB=microbench/variants/NAME.so (tools/quick_bench.py, bench.py).
+# Load one with PLENUM_AMD_LIB=microbench/variants/NAME.so (tests/perf_quick.py, bench.py).
 cd "$(dirname "$0")/../indy-plenum_amd" || exit 1
 SRC="csrc/pv_engine.hip csrc/pv_ingress.hip csrc/host_prep.cpp csrc/signing_json.cpp"
 pids=()

@@ -1,7 +1,7 @@
 """Throughput of the engine on BASELINE config 3 (1M NYM requests, ~2 % adversarial: ~9k extra
 distinct keys from the key-mutating classes) per arithmetic path, device-resident inputs.
-Development/measurement tool (bench.py's headline is config 2):
-    python tools/config3_bench.py [--steps K]"""
+Measurement helper (lives under tests/ because it uses the oracle as the checker; bench.py's headline is config 2):
+    python tests/perf_config3.py [--steps K]"""
 import argparse
 import os
 import sys

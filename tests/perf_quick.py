@@ -1,4 +1,5 @@
-"""Quick device-resident throughput probe (development tool; bench.py is the contract)."""
+"""Quick device-resident throughput probe (measurement helper; under tests/ because it signs with
+the libsodium loader of oracle/; bench.py is the contract)."""
 import ctypes, os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
