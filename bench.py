@@ -236,14 +236,6 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n = args.per_gpu
 
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
-        dist = tdist
-
     t0 = time.perf_counter()
     wire = None
     if args.dataset and os.path.exists(args.dataset):
@@ -255,6 +247,16 @@ def main():
         blob, off, pks = nym_workload.generate(rank * n, n)
     gen_s = time.perf_counter() - t0
     log("rank %d: generated %d requests (%.1f MB) in %.1f s" % (rank, n, blob.nbytes / 1e6, gen_s))
+
+    # the process group (and with it the GPU runtime) comes up only after the forked signing
+    # workers of the workload generator are done: nothing forks once the device is initialised
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
 
     _native.ensure_device(local_rank)
     L = _native.lib()
