@@ -32,6 +32,9 @@ static constexpr int PV_BLOCK = 256;
 #ifndef PV_COMB_A_MINBLOCKS
 #define PV_COMB_A_MINBLOCKS 3
 #endif
+#ifndef PV_FILL_MINBLOCKS
+#define PV_FILL_MINBLOCKS 2
+#endif
 #ifndef PV_MSM_MINBLOCKS
 #define PV_MSM_MINBLOCKS 2  // workgroups per CU the msm kernel's register budget is sized for
 #endif
@@ -764,7 +767,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const ui
 }
 
 // Per (key, position, block of 16 entries): the comb table rows. Grid-stride over nkeys * 256 items.
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_fill_kernel(KeyWork kw, Gate gate) {
+__global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kernel(KeyWork kw, Gate gate) {
     if (!gate.keyed()) return;
     const uint32_t items = kw.nkeys[PV_SPLIT_COMB_KEYS] * PV_COMB_POS * PV_COMB_BLOCKS;
     for (uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x; it < items; it += gridDim.x * PV_BLOCK) {
