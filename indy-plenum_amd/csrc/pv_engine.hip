@@ -330,7 +330,8 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
                                                               const uint32_t* __restrict__ btab_g, Work wk,
                                                               Gate gate) {
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
-    if (blockIdx.x >= ntiles || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;  // before the LDS fill
+    // nothing for this block (or no Straus slot at all): leave before the LDS fill
+    if (blockIdx.x >= ntiles || nc >= n || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
     for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
         reinterpret_cast<uint4*>(sbt)[t] = reinterpret_cast<const uint4*>(btab_g)[t];
