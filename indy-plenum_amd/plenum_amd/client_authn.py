@@ -121,6 +121,62 @@ class SimpleAuthNr(NaclAuthNr):
     def nym_specific_auth(self, request):
         return get_target_verkey(request) if nym_ident_is_dest(request) else None
 
+    def verkey_resolver(self):
+        """A batch-scoped getVerkey: see VerkeyResolver."""
+        return VerkeyResolver(self)
+
+
+_MISS = object()
+_PER_REQUEST = object()
+
+
+class VerkeyResolver:
+    """Batched ``SimpleAuthNr.getVerkey`` (client_authn.py:154-168, request_handlers/utils.py:30-39)
+    for the requests of ONE batch: a DID's registry entry or uncommitted-state NYM record is read
+    and JSON-decoded once per batch instead of once per signature. Only the request-dependent tail
+    (a DID with no record -> the NYM self-verkey rule) runs per request. ``get(idr, request)``
+    returns what ``getVerkey(idr, request)`` returns, or raises ``LookupError`` where getVerkey
+    would raise, so the caller sends that request down the sequential path (which raises the
+    exact exception). Valid while the registry and state do not change (one ingress batch); an
+    authenticator that overrides getVerkey is called per signature, unchanged."""
+
+    def __init__(self, authnr):
+        self.authnr = authnr
+        self.memo = {}  # idr -> verkey | _PER_REQUEST | LookupError
+        self.batched = type(authnr).getVerkey is SimpleAuthNr.getVerkey
+        self.reads = 0
+
+    def _record(self, idr):
+        a = self.authnr
+        try:
+            record = a.clients.get(idr)
+            if not record:
+                self.reads += 1
+                record = get_nym_details(a.state, idr, is_committed=False)
+                if not record:
+                    return _PER_REQUEST
+            return record.get(VERKEY)
+        except Exception as ex:
+            return LookupError(ex)
+
+    def get(self, idr, request):
+        if not self.batched:
+            try:
+                return self.authnr.getVerkey(idr, request)
+            except Exception as ex:
+                raise LookupError(ex)
+        r = self.memo.get(idr, _MISS)
+        if r is _MISS:
+            r = self.memo[idr] = self._record(idr)
+        if r is _PER_REQUEST:
+            try:
+                return self.authnr.get_verkey_specific(request)
+            except Exception as ex:
+                raise LookupError(ex)
+        if isinstance(r, LookupError):
+            raise r
+        return r
+
 
 class CoreAuthMixin:
     excluded_from_signing = {SIGNATURE, SIGNATURES, FEES}
@@ -202,15 +258,23 @@ class CoreAuthMixin:
                         break
                 todo.append((payload, idr, sig, view))
         decoded = b58decode_many([sig for _, _, sig, _ in todo])
+        make_resolver = getattr(self, "verkey_resolver", None)
+        get_verkey = make_resolver().get if make_resolver else self.getVerkey
+        raw_keys = {}  # (verkey, idr) -> DidVerifier's raw key: resolved once per signer per batch
         pairs = []
         for (payload, idr, _, view), raw_sig in zip(todo, decoded):
             if isinstance(raw_sig, Exception):
                 continue
             try:
-                verkey = self.getVerkey(idr, view)
+                verkey = get_verkey(idr, view)
                 if verkey is None:
                     continue
-                key = getattr(verifier(verkey, identifier=idr), "raw_key", None)
+                if verifier is DidVerifier:
+                    key = raw_keys.get((verkey, idr), _MISS)
+                    if key is _MISS:
+                        key = raw_keys[(verkey, idr)] = getattr(verifier(verkey, identifier=idr), "raw_key", None)
+                else:
+                    key = getattr(verifier(verkey, identifier=idr), "raw_key", None)
             except Exception:
                 continue
             if key:

@@ -21,6 +21,7 @@ sequential ``ReqAuthenticator.authenticate`` — with its remaining signature ch
 one more launch — so results, exception classes and messages, and cache side effects are the
 sequential ones.
 """
+import gc
 import json
 import time
 from hashlib import sha256
@@ -166,56 +167,103 @@ def _plain(s):
 
 
 _FAST, _QUERY, _SLOW, _FAILED = 0, 1, 2, 3
+_REQUEST_PARAMS = frozenset(("self",))  # JSON keys Request(**msg) cannot take as keywords
+
+
+def _request_view(msg):
+    """``Request(**msg).as_dict`` for a JSON object, without building the Request (same keys, same
+    insertion order); None when only the Request constructor gives the exact result or exception
+    (not an object, a key colliding with a constructor parameter, plugin fields registered)."""
+    if type(msg) is not dict or PLUGIN_CLIENT_REQUEST_FIELDS or "self" in msg:
+        return None
+    get = msg.get
+    view = {REQ_ID: get(REQ_ID), OPERATION: get(OPERATION)}
+    for name in (IDENTIFIER, SIGNATURES, SIGNATURE, PROTOCOL_VERSION, TAA_ACCEPTANCE, ENDORSER):
+        v = get(name)
+        if v is not None:
+            view[name] = v
+    return view
 
 
 def authenticate_wire_batch(req_authnr, raws, threads=16, timings=None):
     """For each received request (JSON bytes), what the reference's ingress produces at the
     authentication step. Returns [(request dict or None, result)]: result is the identifier set
     ``req_authnr.authenticate(Request(**msg).as_dict, key=Request(**msg).key)`` returns, or the
-    exception instance raised by json.loads, Request(**msg), .key or authenticate."""
+    exception instance raised by json.loads, Request(**msg), .key or authenticate.
+
+    The cyclic garbage collector is paused for the call: the batch allocates a few dicts per
+    request and creates no garbage cycles of its own, and generation scans triggered by those
+    allocations cost as much as the per-request work itself (collection resumes afterwards)."""
+    was_enabled = gc.isenabled()
+    gc.disable()
+    try:
+        return _authenticate_wire_batch(req_authnr, raws, threads, timings)
+    finally:
+        if was_enabled:
+            gc.enable()
+
+
+def _authenticate_wire_batch(req_authnr, raws, threads, timings):
     t0 = time.perf_counter()
     n = len(raws)
     ser_status, mblob, moff, digs = signing_serialize_json(raws, PV_SER_REQUEST, threads)
+    ser_ok = (ser_status == PV_SER_OK).tolist()
+    hexd = digs.tobytes().hex()  # request i's key (Request.digest) = hexd[64 i : 64 i + 64]
     t1 = time.perf_counter()
     authnrs = req_authnr._authenticators
     core = authnrs[0] if authnrs else None
     fast_capable = core is not None and hasattr(core, "_select_signatures") and hasattr(core, "plan_verifications")
-    entries = []  # (kind, msg dict, as_dict, key or exception, sig range)
+    if fast_capable:
+        make_resolver = getattr(core, "verkey_resolver", None)
+        get_verkey = make_resolver().get if make_resolver else _unbatched_get(core)
+        select = core._select_signatures
+    type_kind = {}  # txn type -> _FAST (core alone runs it) / _QUERY / _SLOW, per batch
+    loads = json.loads
+    entries = []  # (kind, msg dict, as_dict, key or exception, identifiers)
     sig_strs, v_msg, v_signer = [], [], []
-    signers, idr_list, vk_list = {}, [], []
+    lo_hi = []  # verification range of each _FAST entry, in entry order
+    signers, idr_list, vk_list, fixed = {}, [], [], {}
     for i, raw in enumerate(raws):
         msg = None
         try:
-            msg = json.loads(raw.decode() if isinstance(raw, (bytes, bytearray)) else raw)
-            req = Request(**msg)
+            msg = loads(raw.decode() if isinstance(raw, (bytes, bytearray)) else raw)
+            view = _request_view(msg)
+            if view is None:
+                req = Request(**msg)
+                view = req.as_dict
+            else:
+                req = None
         except Exception as ex:
             entries.append((_FAILED, msg, None, ex, None))
             continue
-        view = req.as_dict
-        try:
-            key = digs[i].tobytes().hex() if ser_status[i] == PV_SER_OK else req.key
-        except Exception as ex:
-            entries.append((_FAILED, msg, view, ex, None))
-            continue
+        ok_ser = ser_ok[i]
+        if ok_ser:
+            key = hexd[64 * i:64 * i + 64]
+        else:
+            try:
+                key = (req or Request(**msg)).key
+            except Exception as ex:
+                entries.append((_FAILED, msg, view, ex, None))
+                continue
         kind = _SLOW
-        rng = None
-        op = view.get(OPERATION)
-        if fast_capable and ser_status[i] == PV_SER_OK and isinstance(op, dict):
+        ids = None
+        op = view[OPERATION]
+        if fast_capable and ok_ser and type(op) is dict:
             typ = op.get(TXN_TYPE)
-            runners, query = [], False
-            for a in authnrs:
-                if a.is_query(typ):
-                    query = True
-                    break
-                if a.is_write(typ) or a.is_action(typ):
-                    runners.append(a)
-            if query and not runners:
+            try:
+                k = type_kind.get(typ)
+                if k is None:
+                    k = type_kind[typ] = _type_kind(authnrs, core, typ)
+            except TypeError:  # an unhashable type: the sequential path raises for it
+                k = _SLOW
+            if k == _QUERY:
                 kind = _QUERY
-            elif not query and len(runners) == 1 and runners[0] is core:
-                rng = _plan_signatures(core, view, i, sig_strs, v_msg, v_signer, signers, idr_list, vk_list)
-                if rng is not None:
+            elif k == _FAST:
+                ids = _plan_signatures(select, get_verkey, fixed, view, i, sig_strs, v_msg, v_signer, signers, idr_list,
+                                       vk_list, lo_hi)
+                if ids is not None:
                     kind = _FAST
-        entries.append((kind, msg, view, key, rng))
+        entries.append((kind, msg, view, key, ids))
     t2 = time.perf_counter()
     if sig_strs:
         sb, so = _native._blob(sig_strs)
@@ -224,23 +272,30 @@ def authenticate_wire_batch(req_authnr, raws, threads=16, timings=None):
         vp = np.array([v is not None for v in vk_list], np.uint8)
         vstat, verdict = _native.ingress_verify_arrays(sb, so, mblob, moff, np.array(v_msg, np.uint32),
                                                        np.array(v_signer, np.uint32), ib, io, vb, vo, vp)
-        ok = (vstat == 0) & verdict
+        bad = np.zeros(len(sig_strs) + 1, np.int64)
+        np.cumsum(~((vstat == 0) & verdict), out=bad[1:])
+        rng = np.array(lo_hi, np.int64).reshape(-1, 2)
+        fast_ok = iter((bad[rng[:, 1]] == bad[rng[:, 0]]).tolist())
     else:
-        ok = np.zeros(0, bool)
+        fast_ok = iter(())
     t3 = time.perf_counter()
     # requests the fast path cannot finish: their remaining checks in one more launch
     slow_views = []
-    for idx, (kind, msg, view, key, rng) in enumerate(entries):
-        if kind == _FAST and not ok[rng[0]:rng[1]].all():
-            entries[idx] = (_SLOW, msg, view, key, None)
-        if entries[idx][0] == _SLOW:
-            slow_views.append(view)
+    for idx, e in enumerate(entries):
+        kind = e[0]
+        if kind == _FAST and not next(fast_ok):
+            entries[idx] = e = (_SLOW, e[1], e[2], e[3], None)
+            kind = _SLOW
+        if kind == _SLOW:
+            slow_views.append(e[2])
     cache = batch.VerdictCache()
     if slow_views and core is not None and hasattr(core, "plan_verifications"):
         cache.fill(core.plan_verifications(slow_views))
     results = []
+    verified = req_authnr._verified_reqs
+    existing = req_authnr._check_and_verify_existing_req
     with batch.active(cache):
-        for kind, msg, view, key, rng in entries:
+        for kind, msg, view, key, ids in entries:
             if kind == _FAILED:
                 results.append((msg, key))
             elif kind == _SLOW:
@@ -248,13 +303,13 @@ def authenticate_wire_batch(req_authnr, raws, threads=16, timings=None):
                     results.append((msg, req_authnr.authenticate(view, key)))
                 except Exception as ex:
                     results.append((msg, ex))
-            elif key and req_authnr._check_and_verify_existing_req(view, key):
-                results.append((msg, req_authnr._verified_reqs[key]['identifiers']))
+            elif key and existing(view, key):
+                results.append((msg, verified[key]['identifiers']))
             elif kind == _QUERY:
                 results.append((msg, set()))
             else:
-                ids = set(rng[2])
-                req_authnr._verified_reqs[key] = {'signature': view.get(SIGNATURE), 'identifiers': ids}
+                ids = set(ids)
+                verified[key] = {'signature': view.get(SIGNATURE), 'identifiers': ids}
                 results.append((msg, ids))
     t4 = time.perf_counter()
     if timings is not None:
@@ -263,34 +318,68 @@ def authenticate_wire_batch(req_authnr, raws, threads=16, timings=None):
     return results
 
 
-def _plan_signatures(core, view, i, sig_strs, v_msg, v_signer, signers, idr_list, vk_list):
-    """Queue request i's signatures for the device; None when the request needs the sequential
-    path (selection or key lookup raising, non-str fields, a missing key)."""
+def _type_kind(authnrs, core, typ):
+    """How ReqAuthenticator.authenticate (req_authenticator.py:23-51) treats a txn type: _QUERY if
+    an authenticator reports it as a query before any runs, _FAST if the core authenticator is the
+    only one that runs, _SLOW otherwise."""
+    runners = []
+    for a in authnrs:
+        if a.is_query(typ):
+            return _QUERY if not runners else _SLOW
+        if a.is_write(typ) or a.is_action(typ):
+            runners.append(a)
+    return _FAST if len(runners) == 1 and runners[0] is core else _SLOW
+
+
+def _unbatched_get(core):
+    def get(idr, request):
+        try:
+            return core.getVerkey(idr, request)
+        except Exception as ex:
+            raise LookupError(ex)
+    return get
+
+
+def _plan_signatures(select, get_verkey, fixed, view, i, sig_strs, v_msg, v_signer, signers, idr_list, vk_list,
+                     lo_hi):
+    """Queue request i's signatures for the device; returns the identifiers it authenticates, or
+    None when the request needs the sequential path (selection or key lookup raising, non-str
+    fields, a missing key). ``fixed`` maps an identifier whose verkey does not depend on the
+    request (registry or state record, as the batch's VerkeyResolver found) to its signer index."""
     try:
-        sigmap = core._select_signatures(view, None, None)
+        sigmap = select(view, None, None)
     except Exception:
         return None
-    if not isinstance(sigmap, dict) or not sigmap:
+    if type(sigmap) is not dict or not sigmap:
         return None
     staged = []
     for idr, sig in sigmap.items():
-        if not isinstance(sig, str) or not _plain(idr):
+        if type(sig) is not str or type(idr) is not str:
             return None
-        try:
-            vk = core.getVerkey(idr, view)
-        except Exception:
-            return None
-        if vk is None or not _plain(vk):
-            return None
-        staged.append((idr, vk, sig))
-    lo = len(sig_strs)
-    for idr, vk, sig in staged:
-        s = signers.get((idr, vk))
+        s = fixed.get(idr)
         if s is None:
-            s = signers[(idr, vk)] = len(idr_list)
-            idr_list.append(idr.encode())
-            vk_list.append(vk.encode())
+            if not _plain(idr):
+                return None
+            try:
+                vk = get_verkey(idr, view)
+            except Exception:
+                return None
+            if vk is None or not _plain(vk):
+                return None
+            s = signers.get((idr, vk))
+            if s is None:
+                s = signers[(idr, vk)] = len(idr_list)
+                idr_list.append(idr.encode())
+                vk_list.append(vk.encode())
+            memo = getattr(get_verkey, "__self__", None)
+            if memo is not None and getattr(memo, "memo", {}).get(idr) is vk:
+                fixed[idr] = s
+        staged.append((s, sig))
+    lo = len(sig_strs)
+    for s, sig in staged:
         sig_strs.append(sig.rstrip().encode("utf-8", "surrogatepass"))
         v_msg.append(i)
         v_signer.append(s)
-    return lo, len(sig_strs), list(sigmap.keys())
+    lo_hi.append(lo)
+    lo_hi.append(len(sig_strs))
+    return list(sigmap)

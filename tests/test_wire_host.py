@@ -1,0 +1,136 @@
+"""CPU tests of the ingress batch path's host logic (plenum_amd.wire.authenticate_wire_batch) and of
+the batch-scoped verkey resolver. The device launches are replaced by a checker
+that does what pv_ingress_verify / pv_verify_batch compute — base58 decode, DidVerifier key
+resolution, crypto_sign_open — with the host base58 mirror and libsodium 1.0.18 (test
+infrastructure only); tests/test_gpu_wire.py runs the same corpus through the HIP library."""
+import json
+
+import numpy as np
+import pytest
+
+from plenum_amd import _native
+from plenum_amd.base58 import b58decode
+from plenum_amd.client_authn import CoreAuthNr, VerkeyResolver
+from plenum_amd.state_utils import DictState
+from plenum_amd.verifier import DidVerifier
+from test_gpu_wire import Signer, corpus, make_ra, nym, norm, sequential
+
+from plenum_amd import wire
+
+
+@pytest.fixture
+def cpu_engine(sodium, monkeypatch):
+    calls = {"ingress": 0, "sm": 0}
+
+    def ingress(sb, so, mblob, moff, msg_idx, signer_idx, ib, io, vb, vo, vp):
+        calls["ingress"] += 1
+        n = len(so) - 1
+        status, verdict = np.zeros(n, np.uint8), np.zeros(n, bool)
+        for j in range(n):
+            sig = bytes(sb[int(so[j]):int(so[j + 1])])
+            s, m = int(signer_idx[j]), int(msg_idx[j])
+            idr = bytes(ib[int(io[s]):int(io[s + 1])]).decode()
+            vk = bytes(vb[int(vo[s]):int(vo[s + 1])]).decode() if vp[s] else None
+            try:
+                raw_sig = b58decode(sig)
+                pk = DidVerifier(vk, identifier=idr).raw_key
+            except Exception:
+                status[j] = 1
+                continue
+            msg = bytes(mblob[int(moff[m]):int(moff[m + 1])])
+            verdict[j] = sodium.sign_open_ok(raw_sig + msg, pk)
+        return status, verdict
+
+    def sm_batch(blob, off, pks):
+        calls["sm"] += 1
+        return np.array([sodium.sign_open_ok(bytes(blob[int(off[i]):int(off[i + 1])]), bytes(pks[i]))
+                         for i in range(len(off) - 1)], bool)
+
+    monkeypatch.setattr(_native, "ingress_verify_arrays", ingress)
+    monkeypatch.setattr(_native, "verify_sm_batch", sm_batch)
+    return calls
+
+
+def test_wire_batch_matches_sequential_cpu(cpu_engine, sodium):
+    raws, clients, state = corpus(sodium)
+    ra_seq, ra_wire = make_ra(clients, state), make_ra(clients, state)
+    want = [norm(r) for r in sequential(ra_seq, raws)]
+    timings = {}
+    got = [norm(r) for r in wire.authenticate_wire_batch(ra_wire, raws, timings=timings)]
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (i, raws[i][:120], g[1], w[1])
+    assert ra_wire._verified_reqs == ra_seq._verified_reqs
+    assert timings["verifications"] >= 10 and timings["slow"] >= 5
+    assert cpu_engine["ingress"] == 1
+
+
+def test_wire_batch_edge_requests_cpu(cpu_engine, sodium):
+    """JSON the fast view must hand to Request(**msg) itself, unhashable txn types, non-str
+    identifiers, and a batch whose requests repeat a key."""
+    rng = np.random.default_rng(3)
+    s = Signer(sodium, rng.bytes(32))
+    ra_seq, ra_wire = make_ra([s], {}), make_ra([s], {})
+    docs = []
+    d = {"identifier": s.did, "reqId": 1, "operation": nym(1)}
+    d["signature"] = s.sign(d)
+    docs.append(d)
+    docs.append(dict(d, self=1))                                          # Request(**msg) raises TypeError
+    docs.append(dict(d, operation={"type": ["1"]}))                       # unhashable type
+    docs.append(dict(d, operation={"type": {"a": 1}}))
+    docs.append(dict(d, identifier=[s.did]))                              # non-str identifier
+    docs.append(dict(d, identifier=7))
+    docs.append({"reqId": 2, "operation": nym(2), "signatures": {s.did: 5}})  # non-str signature
+    docs.append(dict(d, protocolVersion=None, endorser=None, taaAcceptance=None))
+    raws = [json.dumps(x).encode() for x in docs] + [json.dumps(docs[0]).encode()] * 3
+    want = [norm(r) for r in sequential(ra_seq, raws)]
+    got = [norm(r) for r in wire.authenticate_wire_batch(ra_wire, raws)]
+    assert got == want
+    assert ra_wire._verified_reqs == ra_seq._verified_reqs
+
+
+def test_request_view_matches_request_as_dict():
+    docs = [{"identifier": "a", "reqId": 1, "operation": {"type": "1"}, "signature": "s"},
+            {"reqId": 1, "operation": None, "signatures": {"a": "x"}, "protocolVersion": 2, "endorser": "e",
+             "taaAcceptance": {"t": 1}, "fees": [1], "extra": 3},
+            {"taaAcceptance": 0, "protocolVersion": 0, "identifier": "", "signature": ""},
+            {}]
+    for d in docs:
+        v = wire._request_view(d)
+        r = wire.Request(**d).as_dict
+        assert v == r and list(v) == list(r)
+    assert wire._request_view([1]) is None and wire._request_view({"self": 1}) is None
+
+
+def test_verkey_resolver_reads_each_did_once():
+    """VerkeyResolver.get == getVerkey for registry DIDs, state DIDs, self-creating NYMs, DIDs with
+    no key anywhere, and a state without `get` (getVerkey raises -> LookupError)."""
+    class CountingState(DictState):
+        reads = 0
+
+        def get(self, key, isCommitted=True):
+            CountingState.reads += 1
+            return super().get(key, isCommitted)
+
+    st = CountingState({"StateDid": {"verkey": "~abc"}, "NoKey": {"role": "0"}})
+    core = CoreAuthNr(["1"], [], [], state=st)
+    core.addIdr("Client", "~xyz")
+    reqs = [{"identifier": "Self", "reqId": i, "operation": {"type": "1", "dest": "Self", "verkey": "~v%d" % i}}
+            for i in range(3)]
+    reqs.append({"identifier": "Other", "reqId": 9, "operation": {"type": "1", "dest": "Nobody"}})
+    res = VerkeyResolver(core)
+    for _ in range(4):
+        for idr in ("Client", "StateDid", "NoKey", "Self", "Other"):
+            for r in reqs:
+                assert res.get(idr, r) == core.getVerkey(idr, r)
+    CountingState.reads = 0
+    res = VerkeyResolver(core)
+    for _ in range(10):
+        for r in reqs:
+            res.get("StateDid", r)
+            res.get("Self", r)
+    assert CountingState.reads == 2 and res.reads == 2
+    broken = CoreAuthNr(["1"], [], [], state=None)
+    with pytest.raises(AttributeError):
+        broken.getVerkey("x", reqs[0])
+    with pytest.raises(LookupError):
+        VerkeyResolver(broken).get("x", reqs[0])
