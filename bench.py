@@ -203,6 +203,45 @@ def ingress_leg(n, blob, off, wire, steps, warmup):
     }
 
 
+def config1_python(wire, k=10000):
+    """configs[0] of BASELINE.json: k signed NYM requests through CoreAuthNr.authenticate one at a
+    time on one host core, each signature checked by libsodium 1.0.18 crypto_sign_open (what the
+    reference's node does per request: json.loads -> Request -> ReqAuthenticator.authenticate ->
+    DidVerifier -> libnacl). The drop-in Python classes stand in for the reference's (golden-pinned
+    in tests/test_host_logic.py); libsodium is called through ctypes as libnacl does. CPU leg only."""
+    from oracle.libsodium_ref import LibSodium, find_libsodium
+    from plenum_amd import batch
+    from plenum_amd.client_authn import CoreAuthNr
+    from plenum_amd.req_authenticator import ReqAuthenticator
+    from plenum_amd.wire import Request
+    if find_libsodium() is None:
+        return None
+    sodium = LibSodium()
+    wblob, woff = wire[0], wire[1]
+    k = min(k, len(woff) - 1)
+    pool = nym_workload._pool()
+    core = CoreAuthNr(["1"], ["105"], [], state=None)
+    for p in pool:
+        core.addIdr(p["did"], p["abbr"])
+    ra = ReqAuthenticator()
+    ra.register_authenticator(core)
+    raws = [wblob[int(woff[i]):int(woff[i + 1])].tobytes() for i in range(k)]
+
+    def engine(blob, off, pks):  # one crypto_sign_open per call, as libnacl.crypto_sign_open
+        return [sodium.sign_open_ok(blob.tobytes(), pks[0].tobytes())]
+
+    ok = 0
+    t0 = time.perf_counter()
+    with batch.active(batch.VerdictCache(), engine):
+        for i, raw in enumerate(raws):
+            req = Request(**json.loads(raw.decode()))
+            ok += ra.authenticate(req.as_dict, req.key) == {pool[i % len(pool)]["did"]}
+    dt = time.perf_counter() - t0
+    return {"requests": k, "cores": 1, "requests_per_s": round(k / dt, 1), "us_per_request": round(dt * 1e6 / k, 1),
+            "accepted": ok, "note": "configs[0]: per-request json.loads + Request + ReqAuthenticator.authenticate "
+                                    "(drop-in classes) + libsodium crypto_sign_open, one host thread"}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
@@ -389,6 +428,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(blob, off, pks, min(args.cpu_sample, n), args.cpu_seconds)
         result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+        if wire:
+            c1 = config1_python(wire)
+            if c1:
+                result["cpu_baseline"]["config1_python_authenticate"] = c1
     if rank == 0:
         print(json.dumps(result), flush=True)
     db.free()

@@ -70,10 +70,20 @@ def b58decode_many(values, max_len=512):
 
 
 def b58decode(v):
-    r = b58decode_many([v])[0]
-    if isinstance(r, Exception):
-        raise r
-    return r
+    """One value (the per-signature calls of the sequential path): the same C++ conversion as
+    b58decode_many, called on the bytes directly, without the batch's array packing."""
+    s = _scrub(v)
+    n = len(s)
+    out = ctypes.create_string_buffer(max(n, 1))
+    out_len, status = ctypes.c_uint32(), ctypes.c_uint8()
+    _native.check(_native.lib().pv_b58decode_batch(s, (ctypes.c_uint64 * 2)(0, n), 1, out, max(n, 1),
+                                                   ctypes.byref(out_len), ctypes.byref(status)),
+                  "pv_b58decode_batch")
+    if status.value == 0:
+        return out.raw[:out_len.value]
+    if status.value == 1:
+        raise _invalid_char(s) or ValueError("Invalid character")
+    raise ValueError("base58 output too long")
 
 
 def b58encode(v) -> bytes:

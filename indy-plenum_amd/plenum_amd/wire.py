@@ -167,6 +167,21 @@ def _plain(s):
 
 
 _FAST, _QUERY, _SLOW, _FAILED = 0, 1, 2, 3
+_scan_once = json.JSONDecoder().scan_once  # the C scanner json.loads drives
+
+
+def _loads(raw):
+    """json.loads(raw.decode()) — the same object or the same exception — calling the C scanner
+    directly when the text is exactly one JSON value (no surrounding whitespace); anything else
+    goes through json.loads itself."""
+    s = raw.decode() if isinstance(raw, (bytes, bytearray)) else raw
+    try:
+        obj, end = _scan_once(s, 0)
+        if end == len(s):
+            return obj
+    except (StopIteration, ValueError):
+        pass
+    return json.loads(s)
 _REQUEST_PARAMS = frozenset(("self",))  # JSON keys Request(**msg) cannot take as keywords
 
 
@@ -218,7 +233,6 @@ def _authenticate_wire_batch(req_authnr, raws, threads, timings):
         get_verkey = make_resolver().get if make_resolver else _unbatched_get(core)
         select = core._select_signatures
     type_kind = {}  # txn type -> _FAST (core alone runs it) / _QUERY / _SLOW, per batch
-    loads = json.loads
     entries = []  # (kind, msg dict, as_dict, key or exception, identifiers)
     sig_strs, v_msg, v_signer = [], [], []
     lo_hi = []  # verification range of each _FAST entry, in entry order
@@ -226,7 +240,7 @@ def _authenticate_wire_batch(req_authnr, raws, threads, timings):
     for i, raw in enumerate(raws):
         msg = None
         try:
-            msg = loads(raw.decode() if isinstance(raw, (bytes, bytearray)) else raw)
+            msg = _loads(raw)
             view = _request_view(msg)
             if view is None:
                 req = Request(**msg)

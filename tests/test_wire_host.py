@@ -134,3 +134,35 @@ def test_verkey_resolver_reads_each_did_once():
         broken.getVerkey("x", reqs[0])
     with pytest.raises(LookupError):
         VerkeyResolver(broken).get("x", reqs[0])
+
+
+def test_config1_sequential_and_wire_batch_agree(cpu_engine, sodium):
+    """BASELINE configs[0]: 10k signed NYM requests (the bench template, 1,024 signers) through the
+    per-request path (json.loads -> Request -> ReqAuthenticator.authenticate, one crypto_sign_open
+    per signature) and through authenticate_wire_batch: every request accepted with its signer's
+    DID, identical results and verified-request caches; one engine launch for the batch."""
+    import nym_workload
+    from plenum_amd import batch
+    from plenum_amd.req_authenticator import ReqAuthenticator
+    k = 10000
+    _, _, _, wblob, woff, _, _ = nym_workload.generate_wire(0, k)
+    pool = nym_workload._pool()
+
+    def make():
+        core = CoreAuthNr(["1"], ["105"], [], state=None)
+        for p in pool:
+            core.addIdr(p["did"], p["abbr"])
+        ra = ReqAuthenticator()
+        ra.register_authenticator(core)
+        return ra
+
+    raws = [wblob[int(woff[i]):int(woff[i + 1])].tobytes() for i in range(k)]
+    ra_seq, ra_wire = make(), make()
+    with batch.active(batch.VerdictCache()):
+        want = sequential(ra_seq, raws)
+    assert all(r == {pool[i % len(pool)]["did"]} for i, (_, r) in enumerate(want))
+    assert cpu_engine["sm"] == k and cpu_engine["ingress"] == 0
+    got = wire.authenticate_wire_batch(ra_wire, raws)
+    assert [norm(r) for r in got] == [norm(r) for r in want]
+    assert ra_wire._verified_reqs == ra_seq._verified_reqs
+    assert cpu_engine["ingress"] == 1 and cpu_engine["sm"] == k
