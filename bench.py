@@ -203,6 +203,31 @@ def ingress_leg(n, blob, off, wire, steps, warmup):
     }
 
 
+def multisig_leg(multi, n_req, k, steps):
+    """configs[3]: n_req requests with k signatures each (authenticate_multi, threshold None = all),
+    expanded to one record per (request, signer) and verified in one pv_verify_batch_device call
+    per step; a request is accepted iff all k of its records verify (reduced on the host from the
+    verdict bitmap). Reported beside the headline, never as `value`."""
+    blob, off, pks = multi
+    mb = DeviceBatch(blob, off, pks)
+    mb.verify()  # warm-up
+    _native.check(_native.lib().pv_sync(), "pv_sync")
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        mb.verify()
+    _native.check(_native.lib().pv_sync(), "pv_sync")
+    dt = (time.perf_counter() - t0) / steps
+    path, nkeys = _native.last_path()
+    bits = np.unpackbits(mb.verdict_words().view(np.uint8), bitorder="little")[:n_req * k]
+    accepted = int(bits.reshape(n_req, k).all(axis=1).sum())
+    mb.free()
+    return {"requests": n_req, "signatures_per_request": k, "verifies_per_s": round(n_req * k / dt, 1),
+            "requests_per_s": round(n_req / dt, 1), "ms_per_step": round(dt * 1e3, 3), "steps": steps,
+            "distinct_keys": nkeys, "requests_accepted": accepted, "verdicts_ok": accepted == n_req,
+            "note": "configs[3]: 1 author + 2 endorsers over the same payload, records request-major, "
+                    "device-resident, one launch per step"}
+
+
 def config1_python(wire, k=10000):
     """configs[0] of BASELINE.json: k signed NYM requests through CoreAuthNr.authenticate one at a
     time on one host core, each signature checked by libsodium 1.0.18 crypto_sign_open (what the
@@ -268,6 +293,7 @@ def main():
     ap.add_argument("--no-straus", action="store_true", help="skip the secondary Straus-path measurement")
     ap.add_argument("--dataset", default=None, help="npz from tools/nym_workload.py (profiling runs: no fork)")
     ap.add_argument("--no-ingress", action="store_true", help="skip the ingress / host-serialization measurements")
+    ap.add_argument("--no-multisig", action="store_true", help="skip the configs[3] multi-signature measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -286,6 +312,11 @@ def main():
         blob, off, pks = nym_workload.generate(rank * n, n)
     gen_s = time.perf_counter() - t0
     log("rank %d: generated %d requests (%.1f MB) in %.1f s" % (rank, n, blob.nbytes / 1e6, gen_s))
+    multi = None
+    if world == 1 and not args.no_multisig and not args.dataset:
+        t0 = time.perf_counter()
+        multi = nym_workload.generate_multisig(0, n, 3)  # before the device comes up (forked signers)
+        log("rank %d: generated %d 3-signature requests in %.1f s" % (rank, n, time.perf_counter() - t0))
 
     # the process group (and with it the GPU runtime) comes up only after the forked signing
     # workers of the workload generator are done: nothing forks once the device is initialised
@@ -423,6 +454,8 @@ def main():
         result["host_path"] = {"verifies_per_s": round(hsamp / dt, 1), "requests": hsamp, "ok": bool(v.all())}
         result["host_prep"] = {"workload_generation_s": round(gen_s, 2), "note": "serialize + sign, %d workers" % min(
             16, os.cpu_count() or 1)}
+    if multi is not None:
+        result["multisig"] = multisig_leg(multi, n, 3, max(3, args.steps // 4))
     if rank == 0 and world == 1 and wire:
         result["ingress"] = ingress_leg(n, blob, off, wire, max(3, args.steps // 4), 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

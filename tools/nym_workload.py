@@ -115,6 +115,43 @@ def _sign_range(args):
     return b"".join(out_sm), [len(x) for x in out_sm], b"".join(out_pk), extra
 
 
+def endorsers(i, k=3):
+    """Signers of multi-signature request i (configs[3]): its author and k - 1 endorsers."""
+    return [(i + 341 * j) % POOL for j in range(k)]
+
+
+def _sign_multi_range(args):
+    lo, hi, k = args
+    pool = _pool()
+    lib = sodium()
+    sig = ctypes.create_string_buffer(64)
+    out_sm, out_pk = [], []
+    for i in range(lo, hi):
+        m = message(i, pool[i % POOL])  # the payload every signer signs (serializeForSig ignores the signer)
+        for s in endorsers(i, k):
+            lib.crypto_sign_detached(sig, None, m, ctypes.c_ulonglong(len(m)), pool[s]["sk"])
+            out_sm.append(sig.raw + m)
+            out_pk.append(pool[s]["vk"])
+    return b"".join(out_sm), [len(x) for x in out_sm], b"".join(out_pk)
+
+
+def generate_multisig(lo, n, k=3, workers=None):
+    """configs[3]: requests [lo, lo + n) with k signatures each over the same payload, expanded to
+    one (sig || msg, pk) record per (request, signer), request-major."""
+    workers = workers or min(16, max(1, (os.cpu_count() or 1)))
+    chunk = max(1, (n + workers * 4 - 1) // (workers * 4))
+    ranges = [(a, min(a + chunk, lo + n), k) for a in range(lo, lo + n, chunk)]
+    if workers > 1 and n > 20000:
+        with mp.get_context("fork").Pool(workers) as p:
+            parts = p.map(_sign_multi_range, ranges)
+    else:
+        parts = [_sign_multi_range(r) for r in ranges]
+    blob = np.frombuffer(b"".join(p[0] for p in parts), dtype=np.uint8)
+    off = _offsets([x for p in parts for x in p[1]])
+    pks = np.frombuffer(b"".join(p[2] for p in parts), dtype=np.uint8).reshape(n * k, 32)
+    return blob, off, pks
+
+
 def _offsets(lens):
     off = np.zeros(len(lens) + 1, dtype=np.uint64)
     np.cumsum(np.asarray(lens, dtype=np.uint64), out=off[1:])
