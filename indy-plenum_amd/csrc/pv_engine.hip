@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <mutex>
 #include <random>
+#include <atomic>
 #include <thread>
 #include <string>
 #include <vector>
@@ -1362,23 +1363,33 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
     return launch(d_sm, d_off, n, d_pk, d_verdict_words, stream ? (hipStream_t)stream : g_ctx.stream);
 }
 
-// Copy into the pinned staging buffer on several host threads: one thread moves ~10 GB/s, and the
-// request blob of a large host-buffer batch is hundreds of MB (the copy dominated pv_verify_batch).
-static void pv_parallel_memcpy(uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+// Move the request blob host -> pinned staging -> HBM. One host thread copies ~10 GB/s and the blob of
+// a large host-buffer batch is hundreds of MB, so up to 8 threads each take a contiguous slice and
+// copy it in 4 MB pieces, enqueueing each piece's DMA (hipMemcpyAsync from pinned memory) as soon as
+// it is staged: the PCIe transfer of earlier pieces overlaps the staging copy of later ones. The
+// pieces are disjoint, so their order on the stream does not matter; the kernels launched on the
+// same stream afterwards see every piece.
+static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* src, uint64_t bytes, hipStream_t s) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const unsigned nt = bytes < (8ull << 20) ? 1u : std::min(8u, hw);
-    if (nt == 1) {
-        memcpy(dst, src, bytes);
-        return;
-    }
+    const uint64_t piece = 4ull << 20;
+    std::atomic<int> err{0};
+    auto work = [&](uint64_t a, uint64_t b) {
+        for (uint64_t o = a; o < b; o += piece) {
+            const uint64_t e = std::min(b, o + piece);
+            memcpy(h_stage + o, src + o, e - o);
+            if (hipMemcpyAsync(d_dst + o, h_stage + o, e - o, hipMemcpyHostToDevice, s) != hipSuccess) err = 1;
+        }
+    };
     const uint64_t per = (bytes + nt - 1) / nt;
     std::vector<std::thread> th;
     for (unsigned t = 1; t < nt; t++) {
         const uint64_t a = std::min<uint64_t>(bytes, t * per), b = std::min<uint64_t>(bytes, a + per);
-        if (b > a) th.emplace_back([=] { memcpy(dst + a, src + a, b - a); });
+        if (b > a) th.emplace_back(work, a, b);
     }
-    memcpy(dst, src, std::min<uint64_t>(bytes, per));
+    work(0, std::min<uint64_t>(bytes, per));
     for (auto& x : th) x.join();
+    return err.load() ? fail(PV_ERR_LAUNCH, "hipMemcpyAsync (request blob) failed") : PV_OK;
 }
 
 int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
@@ -1403,13 +1414,17 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     uint64_t* hoff = reinterpret_cast<uint64_t*>(h + pk_bytes);
     for (uint64_t i = 0; i <= n; i++) hoff[i] = sm_off[i] - sm_off[0];
     uint8_t* hblob = h + pk_bytes + off_bytes + v_bytes;
-    pv_parallel_memcpy(hblob, sm + sm_off[0], blob);
     memset(hblob + blob, 0, PV_BLOB_SLACK);
     uint8_t* d = g_ctx.d_stage;
+    uint8_t* dblob = d + pk_bytes + off_bytes + v_bytes;
     hipStream_t s = g_ctx.stream;
     PV_HIP(hipMemcpyAsync(d, h, pk_bytes + off_bytes, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-    PV_HIP(hipMemcpyAsync(d + pk_bytes + off_bytes + v_bytes, hblob, blob + PV_BLOB_SLACK,
-                          hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    PV_HIP(hipMemcpyAsync(dblob + blob, hblob + blob, PV_BLOB_SLACK, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    rc = pv_stage_to_device(dblob, hblob, sm + sm_off[0], blob, s);
+    if (rc) {
+        (void)hipStreamSynchronize(s);  // no DMA may still read the staging buffer when the caller retries
+        return rc;
+    }
     uint64_t* dver = reinterpret_cast<uint64_t*>(d + pk_bytes + off_bytes);
     rc = launch(d + pk_bytes + off_bytes + v_bytes, reinterpret_cast<const uint64_t*>(d + pk_bytes), n, d, dver, s);
     if (rc) return rc;
