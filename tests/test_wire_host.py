@@ -166,3 +166,22 @@ def test_config1_sequential_and_wire_batch_agree(cpu_engine, sodium):
     assert [norm(r) for r in got] == [norm(r) for r in want]
     assert ra_wire._verified_reqs == ra_seq._verified_reqs
     assert cpu_engine["ingress"] == 1 and cpu_engine["sm"] == k
+
+
+@pytest.mark.parametrize("raw", [b'{"a": 1}', b' {"a": 1}', b'{"a": 1} ', b'{"a": 1}\n', b'\xef\xbb\xbf{"a": 1}',
+                                 b'{"a": NaN, "b": -Infinity}', b'[1, 2]', b'"text"', b'12', b'12 34', b'{"a": 1}{}',
+                                 b'{"a": "\\u00e9\\ud83d\\ude00"}', b'{"a": "\x01"}', b'\xff\xfe', b'', b'   ',
+                                 b'{"a": 1,}', b'{"a": [' * 3 + b']}' * 3, '{"é": 1}'.encode()])
+def test_loads_matches_json_loads(raw):
+    """wire._loads is json.loads(raw.decode()): same object or same exception class and message."""
+    def outcome(fn):
+        try:
+            return ("ok", fn(raw))
+        except Exception as ex:
+            return ("exc", type(ex).__name__, str(ex))
+    a = outcome(wire._loads)
+    b = outcome(lambda r: json.loads(r.decode()))
+    if a[0] == "ok" and b[0] == "ok":
+        assert json.dumps(a[1]) == json.dumps(b[1])
+    else:
+        assert a == b
