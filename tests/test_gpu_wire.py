@@ -169,3 +169,32 @@ def test_wire_batch_many_valid_requests(native, sodium):
             assert r == {signers[i % 64].did}, (i, r)
     assert timings["slow"] == sum(altered)
     assert len(ra._verified_reqs) == len(raws) - sum(altered)
+
+
+def check_request_dependent_verkeys(sodium):
+    """A DID with no registry or state record creating itself: its verkey comes from each
+    request's own operation (NYM self-verkey rule), so it must not be shared across the batch —
+    the same DID sends NYMs carrying its right key, another signer's key, and no key; a state DID
+    signs many requests (one state read per batch)."""
+    rng = np.random.default_rng(21)
+    me, other, st = (Signer(sodium, rng.bytes(32)) for _ in range(3))
+    ra_seq, ra_wire = make_ra([], {st.did: {"verkey": st.verkey}}), make_ra([], {st.did: {"verkey": st.verkey}})
+    docs = []
+    for i, vk in enumerate([me.verkey, other.verkey, None, me.verkey, other.verkey]):
+        d = {"identifier": me.did, "reqId": 100 + i, "operation": nym(100 + i, dest=me.did, verkey=vk)}
+        d["signature"] = me.sign(d)
+        docs.append(d)
+    for i in range(20):
+        d = {"identifier": st.did, "reqId": 200 + i, "operation": nym(200 + i)}
+        d["signature"] = st.sign(d)
+        docs.append(d)
+    raws = [json.dumps(x).encode() for x in docs]
+    want = [norm(r) for r in sequential(ra_seq, raws)]
+    got = [norm(r) for r in authenticate_wire_batch(ra_wire, raws)]
+    assert got == want
+    assert [w[1][0] for w in want[:5]] == ["ok", "exc", "exc", "ok", "exc"]
+    assert ra_wire._verified_reqs == ra_seq._verified_reqs
+
+
+def test_wire_batch_request_dependent_verkeys(native, sodium):
+    check_request_dependent_verkeys(sodium)

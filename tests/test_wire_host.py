@@ -13,7 +13,7 @@ from plenum_amd.base58 import b58decode
 from plenum_amd.client_authn import CoreAuthNr, VerkeyResolver
 from plenum_amd.state_utils import DictState
 from plenum_amd.verifier import DidVerifier
-from test_gpu_wire import Signer, corpus, make_ra, nym, norm, sequential
+from test_gpu_wire import Signer, check_request_dependent_verkeys, corpus, make_ra, nym, norm, sequential
 
 from plenum_amd import wire
 
@@ -86,6 +86,10 @@ def test_wire_batch_edge_requests_cpu(cpu_engine, sodium):
     got = [norm(r) for r in wire.authenticate_wire_batch(ra_wire, raws)]
     assert got == want
     assert ra_wire._verified_reqs == ra_seq._verified_reqs
+
+
+def test_wire_batch_request_dependent_verkeys_cpu(cpu_engine, sodium):
+    check_request_dependent_verkeys(sodium)
 
 
 def test_request_view_matches_request_as_dict():
