@@ -219,7 +219,10 @@ PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const 
 // masks its verdict. `src` streams the points: src.z(t, Z) and src.xy(t, X, Y) may be called more
 // than once for the same t (the device reloads instead of holding 8 points in registers), and
 // sink(t, enc, use) receives each encoding in descending t.
-static constexpr int PV_ENC_BATCH = 8;
+#ifndef PV_ENC_BATCH_N
+#define PV_ENC_BATCH_N 8
+#endif
+static constexpr int PV_ENC_BATCH = PV_ENC_BATCH_N;
 template <class Src, class Sink>
 PV_HD void pv_encode_batch_stream(const Src& src, bool use[PV_ENC_BATCH], const Sink& sink) {
     fe c[PV_ENC_BATCH];
