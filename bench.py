@@ -484,6 +484,20 @@ def main():
         v = _native.verify_sm_batch(blob[:int(hoff[-1])], hoff, pks[:hsamp])
         dt = time.perf_counter() - t1
         result["host_path"] = {"verifies_per_s": round(hsamp / dt, 1), "requests": hsamp, "ok": bool(v.all())}
+        # latency of one host-buffer call at the batch sizes Plenum's feed points produce (a ZStack
+        # client quota is 100 messages, a node quota 1,000): median of 20 calls
+        lat = {}
+        for k in (100, 1000, 10000):
+            ko = off[:k + 1]
+            kb, kp = blob[:int(ko[-1])], pks[:k]
+            _native.verify_sm_batch(kb, ko, kp)
+            ts, okk = [], True
+            for _ in range(20):
+                t1 = time.perf_counter()
+                okk &= bool(_native.verify_sm_batch(kb, ko, kp).all())
+                ts.append(time.perf_counter() - t1)
+            lat[str(k)] = {"median_ms": round(1e3 * float(np.median(ts)), 3), "ok": okk}
+        result["host_path"]["batch_latency"] = lat
         result["host_prep"] = {"workload_generation_s": round(gen_s, 2), "note": "serialize + sign, %d workers" % min(
             16, os.cpu_count() or 1)}
     if multi is not None:
