@@ -200,11 +200,18 @@ def _request_view(msg):
     return view
 
 
-def authenticate_wire_batch(req_authnr, raws, threads=16, timings=None):
+def authenticate_wire_batch(req_authnr, raws, threads=16, timings=None, one_call_per_request=False):
     """For each received request (JSON bytes), what the reference's ingress produces at the
     authentication step. Returns [(request dict or None, result)]: result is the identifier set
     ``req_authnr.authenticate(Request(**msg).as_dict, key=Request(**msg).key)`` returns, or the
     exception instance raised by json.loads, Request(**msg), .key or authenticate.
+
+    By default a request whose signatures all verify on the device completes without calling
+    ``req_authnr.authenticate`` (zero calls; the verified-request cache is filled as authenticate
+    fills it). ``one_call_per_request=True`` keeps the reference's call pattern — authenticate
+    exactly once per request that is not a cache hit (the spy of
+    plenum/test/node_request/test_propagate/test_no_reauth.py:11-23) — with every signature check
+    of the batch still in one launch.
 
     The cyclic garbage collector is paused for the call: the batch allocates a few dicts per
     request and creates no garbage cycles of its own, and generation scans triggered by those
@@ -212,13 +219,13 @@ def authenticate_wire_batch(req_authnr, raws, threads=16, timings=None):
     was_enabled = gc.isenabled()
     gc.disable()
     try:
-        return _authenticate_wire_batch(req_authnr, raws, threads, timings)
+        return _authenticate_wire_batch(req_authnr, raws, threads, timings, one_call_per_request)
     finally:
         if was_enabled:
             gc.enable()
 
 
-def _authenticate_wire_batch(req_authnr, raws, threads, timings):
+def _authenticate_wire_batch(req_authnr, raws, threads, timings, one_call_per_request=False):
     t0 = time.perf_counter()
     n = len(raws)
     ser_status, mblob, moff, digs = signing_serialize_json(raws, PV_SER_REQUEST, threads)
@@ -227,7 +234,8 @@ def _authenticate_wire_batch(req_authnr, raws, threads, timings):
     t1 = time.perf_counter()
     authnrs = req_authnr._authenticators
     core = authnrs[0] if authnrs else None
-    fast_capable = core is not None and hasattr(core, "_select_signatures") and hasattr(core, "plan_verifications")
+    fast_capable = (not one_call_per_request and core is not None and hasattr(core, "_select_signatures")
+                    and hasattr(core, "plan_verifications"))
     if fast_capable:
         make_resolver = getattr(core, "verkey_resolver", None)
         get_verkey = make_resolver().get if make_resolver else _unbatched_get(core)

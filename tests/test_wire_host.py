@@ -189,3 +189,31 @@ def test_loads_matches_json_loads(raw):
         assert json.dumps(a[1]) == json.dumps(b[1])
     else:
         assert a == b
+
+
+def test_wire_batch_one_call_per_request_cpu(cpu_engine, sodium):
+    """one_call_per_request=True: the reference's call pattern (ReqAuthenticator.authenticate ->
+    CoreAuthNr.authenticate once per request that is not a verified-cache hit; test_no_reauth's
+    spy), identical results, every signature check in one launch."""
+    raws, clients, state = corpus(sodium)
+    ra_seq, ra_wire = make_ra(clients, state), make_ra(clients, state)
+    counts = {"seq": 0, "wire": 0}
+
+    def spy(ra, tag):
+        core = ra._authenticators[0]
+        orig = core.authenticate
+
+        def counted(*a, **kw):
+            counts[tag] += 1
+            return orig(*a, **kw)
+        core.authenticate = counted
+
+    spy(ra_seq, "seq")
+    spy(ra_wire, "wire")
+    want = [norm(r) for r in sequential(ra_seq, raws)]
+    cpu_engine["sm"] = 0
+    got = [norm(r) for r in wire.authenticate_wire_batch(ra_wire, raws, one_call_per_request=True)]
+    assert got == want
+    assert ra_wire._verified_reqs == ra_seq._verified_reqs
+    assert counts["wire"] == counts["seq"] > 10
+    assert cpu_engine["sm"] == 1  # the plan's one launch; nothing verified one by one
