@@ -39,6 +39,9 @@ static constexpr int PV_BLOCK = 256;
 #ifndef PV_MSM_MINBLOCKS
 #define PV_MSM_MINBLOCKS 2  // workgroups per CU the msm kernel's register budget is sized for
 #endif
+#ifndef PV_PREP_MINBLOCKS
+#define PV_PREP_MINBLOCKS 2  // Straus prep (decompression + SHA-512 + recoding)
+#endif
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
 static constexpr uint64_t PV_KEYED_MIN = 32768;   // AUTO: smaller chunks skip dedup (Straus only)
@@ -290,7 +293,7 @@ __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, con
 }
 
 // Kernel 1 (Straus path): pv_prep_slot over the Straus slots.
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_prep_kernel(const uint8_t* __restrict__ sm,
+__global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(const uint8_t* __restrict__ sm,
                                                                const uint64_t* __restrict__ off, uint64_t n,
                                                                const uint8_t* __restrict__ pk, Work wk, Gate gate) {
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
