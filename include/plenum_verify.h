@@ -71,7 +71,9 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
 /* Device buffers in, device bitmap out. Requirements: d_sm 4-byte aligned and readable up to
  * sm_off[n] + PV_BLOB_SLACK (records themselves need no alignment), d_pk 16-byte aligned,
  * verdict_words holds ceil(n/64) 64-bit words. Enqueued on `stream` (a hipStream_t, NULL = the
- * library stream); returns without synchronising. */
+ * library stream); returns without synchronising. Thread-safe: calls are serialised on a library
+ * mutex, and a call on a different stream than the previous call first makes its stream wait for
+ * the previous launch (the workspace is shared), so concurrent callers get correct verdicts. */
 int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
                            uint64_t* d_verdict_words, void* stream);
 
@@ -167,8 +169,9 @@ int pv_resolve_verkeys(const char* idr_chars, const uint64_t* idr_off, const cha
  *   3       msg_idx / signer_idx out of range, or msg_bytes_total too small (verdict 0)
  *   16 + k  signer key resolution status k (pv_resolve_verkeys codes; k = 3: no key, verify() is
  *           False) — the verdict bit is 0
- * Enqueued on `stream` (NULL = the library stream); workspace is the library's, so concurrent calls
- * must share one stream. pv_ingress_verify is the same on host buffers (synchronous; validates
+ * Enqueued on `stream` (NULL = the library stream); the workspace is the library's and is handed
+ * over between streams as for pv_verify_batch_device, so calls on different streams and threads are
+ * safe. pv_ingress_verify is the same on host buffers (synchronous; validates
  * offsets and indices and returns PV_ERR_ARG instead of launching on bad input).
  * pv_ingress_front_ms: device time of the most recent call's front end (decode, resolve, scan,
  * assembly), excluding the verification kernels. */
@@ -230,6 +233,13 @@ int pv_dev_free(void* p);
 int pv_memcpy_h2d(void* dst, const void* src, uint64_t bytes);
 int pv_memcpy_d2h(void* dst, const void* src, uint64_t bytes);
 int pv_sync(void);
+/* Caller streams for the *_device entry points, for hosts without a GPU framework. A stream handed
+ * to pv_verify_batch_device / pv_ingress_verify_device may be any stream of this device: batches
+ * enqueued on DIFFERENT streams are ordered by the library (each launch waits for the previous one
+ * to release the shared workspace), so they never race; pv_stream_destroy synchronises first. */
+int pv_stream_create(void** stream);
+int pv_stream_destroy(void* stream);
+int pv_stream_sync(void* stream);
 
 #ifdef __cplusplus
 }

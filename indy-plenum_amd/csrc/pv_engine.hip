@@ -985,6 +985,11 @@ struct Ctx {
     hipEvent_t ev_tables_ready = nullptr;    // comb tables done (kstream -> main)
     hipStream_t sstream = nullptr;           // Straus-path slots of a split chunk, overlapped
     hipEvent_t ev_straus_done = nullptr;     // their q / flags written (sstream -> main)
+    // Workspace hand-over between callers' streams: every launch ends by recording ev_launch_done
+    // on its stream; a launch on a DIFFERENT stream first makes its stream wait for it, so two
+    // batches enqueued on two caller streams never share the workspace at the same time.
+    hipEvent_t ev_launch_done = nullptr;
+    hipStream_t last_stream = nullptr;
     uint32_t* d_btab = nullptr;
     Work work{nullptr, nullptr, nullptr, nullptr, 0};
     KeyWork kw{};
@@ -1048,10 +1053,25 @@ int ensure_events(int count) {
     return PV_OK;
 }
 
-// Chunks of at most work.stride requests (a multiple of 64, so verdict words never straddle).
+int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk, uint64_t* d_verdict,
+                  hipStream_t stream);
+
+// One batch on `stream` (caller holds g_mu). Chunks of at most work.stride requests (a multiple of
+// 64, so verdict words never straddle).
 int launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk, uint64_t* d_verdict,
            hipStream_t stream) {
     if (n == 0) return PV_OK;
+    if (g_ctx.last_stream && g_ctx.last_stream != stream)
+        PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_launch_done, 0), PV_ERR_LAUNCH);
+    int rc = launch_chunks(d_sm, d_off, n, d_pk, d_verdict, stream);
+    // recorded even after a failed enqueue: whatever did get enqueued is covered
+    PV_HIP(hipEventRecord(g_ctx.ev_launch_done, stream), PV_ERR_LAUNCH);
+    g_ctx.last_stream = stream;
+    return rc;
+}
+
+int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk, uint64_t* d_verdict,
+                  hipStream_t stream) {
     const uint64_t cap = g_ctx.work.stride;
     const int nchunks = (int)((n + cap - 1) / cap);
     constexpr int NE = PV_NSTAGES + 1;
@@ -1213,6 +1233,7 @@ int pv_init(int device) {
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     std::vector<uint32_t> bt(PV_BTAB_ENTRIES * PV_BTAB_STRIDE);
     pv_build_b_table(bt.data());
     PV_HIP(hipMalloc((void**)&g_ctx.d_btab, bt.size() * 4), PV_ERR_ALLOC);
@@ -1290,10 +1311,12 @@ void pv_shutdown(void) {
     if (g_ctx.ev_tables_ready) (void)hipEventDestroy(g_ctx.ev_tables_ready);
     if (g_ctx.sstream) (void)hipStreamDestroy(g_ctx.sstream);
     if (g_ctx.ev_straus_done) (void)hipEventDestroy(g_ctx.ev_straus_done);
+    if (g_ctx.ev_launch_done) (void)hipEventDestroy(g_ctx.ev_launch_done);
     g_ctx = Ctx();
 }
 
 int pv_last_path(int* path, uint32_t* nkeys) {
+    std::lock_guard<std::mutex> lk(g_mu);
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_last_path: call pv_init first");
     uint32_t u[4] = {0, 0, 0, 0};
     if (g_ctx.last_keyed) {
@@ -1310,6 +1333,7 @@ int pv_last_path(int* path, uint32_t* nkeys) {
 }
 
 int pv_last_split(uint32_t* keys, uint32_t* comb_keys, uint32_t* comb_requests) {
+    std::lock_guard<std::mutex> lk(g_mu);
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_last_split: call pv_init first");
     if (keys) *keys = g_ctx.last_split[0];
     if (comb_keys) *comb_keys = g_ctx.last_split[1];
@@ -1320,17 +1344,20 @@ int pv_last_split(uint32_t* keys, uint32_t* comb_keys, uint32_t* comb_requests) 
 int pv_set_path(int mode) {
     if (mode != PV_PATH_AUTO && mode != PV_PATH_STRAUS && mode != PV_PATH_COMB)
         return fail(PV_ERR_ARG, "pv_set_path: unknown mode");
+    std::lock_guard<std::mutex> lk(g_mu);
     g_ctx.path = mode;
     return PV_OK;
 }
 
 int pv_set_timing(int enable) {
+    std::lock_guard<std::mutex> lk(g_mu);
     g_ctx.timing = enable != 0;
     g_ctx.ev_used = 0;
     return PV_OK;
 }
 
 int pv_stage_times(double* ms, int max_stages, int* launches) {
+    std::lock_guard<std::mutex> lk(g_mu);
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_stage_times: call pv_init first");
     constexpr int NE = PV_NSTAGES + 1;
     double acc[PV_NSTAGES] = {0};
@@ -1363,6 +1390,7 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
                            uint64_t* d_verdict_words, void* stream) {
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_verify_batch_device: call pv_init first");
     if (n > 0 && (!d_sm || !d_off || !d_pk || !d_verdict_words)) return fail(PV_ERR_ARG, "null pointer");
+    std::lock_guard<std::mutex> lk(g_mu);
     return launch(d_sm, d_off, n, d_pk, d_verdict_words, stream ? (hipStream_t)stream : g_ctx.stream);
 }
 
@@ -1489,6 +1517,29 @@ int pv_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
 }
 int pv_sync(void) {
     PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
+    return PV_OK;
+}
+int pv_stream_create(void** stream) {
+    if (!stream) return fail(PV_ERR_ARG, "pv_stream_create: null pointer");
+    hipStream_t s = nullptr;
+    PV_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+    *stream = (void*)s;
+    return PV_OK;
+}
+int pv_stream_destroy(void* stream) {
+    if (!stream) return PV_OK;
+    PV_HIP(hipStreamSynchronize((hipStream_t)stream), PV_ERR_LAUNCH);
+    {
+        // a later launch must not wait on an event of a destroyed stream
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (g_ctx.last_stream == (hipStream_t)stream) g_ctx.last_stream = nullptr;
+    }
+    pv_ingress_forget_stream(stream);
+    PV_HIP(hipStreamDestroy((hipStream_t)stream), PV_ERR_LAUNCH);
+    return PV_OK;
+}
+int pv_stream_sync(void* stream) {
+    PV_HIP(hipStreamSynchronize(stream ? (hipStream_t)stream : g_ctx.stream), PV_ERR_LAUNCH);
     return PV_OK;
 }
 

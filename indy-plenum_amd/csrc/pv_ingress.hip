@@ -468,6 +468,9 @@ struct IngWork {
     uint8_t* blob = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    // workspace hand-over between callers' streams (as the engine's ev_launch_done)
+    hipEvent_t ev_done = nullptr;
+    hipStream_t last_stream = nullptr;
     // host-entry staging (pv_ingress_verify)
     uint8_t* h_stage = nullptr;
     uint64_t h_cap = 0;
@@ -518,10 +521,18 @@ int ensure_work(uint64_t n, uint64_t nsig, uint64_t blob_bytes) {
     if (!g_ing.ev0) {
         ING_HIP(hipEventCreate(&g_ing.ev0), PV_ERR_NO_DEVICE);
         ING_HIP(hipEventCreate(&g_ing.ev1), PV_ERR_NO_DEVICE);
+        ING_HIP(hipEventCreateWithFlags(&g_ing.ev_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     }
     return PV_OK;
 }
 
+int ingress_enqueue(const uint8_t* sig_chars, const uint64_t* sig_off, const uint32_t* msg_idx,
+                    const uint32_t* signer_idx, uint64_t n, const uint8_t* msg, const uint64_t* msg_off, uint64_t nmsg,
+                    uint64_t cap, const uint8_t* idr_chars, const uint64_t* idr_off, const uint8_t* vk_chars,
+                    const uint64_t* vk_off, const uint8_t* vk_present, uint64_t nsig, uint8_t* status,
+                    uint64_t* verdict, hipStream_t s);
+
+// Caller holds g_ing_mu.
 int ingress_device(const uint8_t* sig_chars, const uint64_t* sig_off, const uint32_t* msg_idx,
                    const uint32_t* signer_idx, uint64_t n, const uint8_t* msg, const uint64_t* msg_off, uint64_t nmsg,
                    uint64_t msg_bytes_total, const uint8_t* idr_chars, const uint64_t* idr_off,
@@ -532,6 +543,19 @@ int ingress_device(const uint8_t* sig_chars, const uint64_t* sig_off, const uint
     const uint64_t cap = 96 * n + msg_bytes_total;
     int rc = ensure_work(n, nsig, cap);
     if (rc) return rc;
+    if (g_ing.last_stream && g_ing.last_stream != s) ING_HIP(hipStreamWaitEvent(s, g_ing.ev_done, 0), PV_ERR_LAUNCH);
+    rc = ingress_enqueue(sig_chars, sig_off, msg_idx, signer_idx, n, msg, msg_off, nmsg, cap, idr_chars, idr_off,
+                         vk_chars, vk_off, vk_present, nsig, status, verdict, s);
+    ING_HIP(hipEventRecord(g_ing.ev_done, s), PV_ERR_LAUNCH);
+    g_ing.last_stream = s;
+    return rc;
+}
+
+int ingress_enqueue(const uint8_t* sig_chars, const uint64_t* sig_off, const uint32_t* msg_idx,
+                    const uint32_t* signer_idx, uint64_t n, const uint8_t* msg, const uint64_t* msg_off, uint64_t nmsg,
+                    uint64_t cap, const uint8_t* idr_chars, const uint64_t* idr_off, const uint8_t* vk_chars,
+                    const uint64_t* vk_off, const uint8_t* vk_present, uint64_t nsig, uint8_t* status,
+                    uint64_t* verdict, hipStream_t s) {
     ING_HIP(hipEventRecord(g_ing.ev0, s), PV_ERR_LAUNCH);
     if (nsig > 0) {
         hipLaunchKernelGGL(pv_ing_signer_kernel, dim3((unsigned)((nsig + ING_BLOCK - 1) / ING_BLOCK)), dim3(ING_BLOCK),
@@ -562,6 +586,11 @@ int ingress_device(const uint8_t* sig_chars, const uint64_t* sig_off, const uint
 }
 
 }  // namespace
+
+void pv_ingress_forget_stream(void* stream) {
+    std::lock_guard<std::mutex> lk(g_ing_mu);
+    if (g_ing.last_stream == (hipStream_t)stream) g_ing.last_stream = nullptr;
+}
 
 extern "C" {
 

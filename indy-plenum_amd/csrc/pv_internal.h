@@ -10,5 +10,7 @@
 hipStream_t pv_engine_stream();
 // Records `msg` as the calling thread's pv_last_error() and returns `code`.
 int pv_fail(int code, const std::string& msg);
+// A caller stream is being destroyed: the ingress workspace stops handing over through it.
+void pv_ingress_forget_stream(void* stream);
 
 #endif  // PV_INTERNAL_H

@@ -19,6 +19,7 @@ PV_ABI_VERSION = 1
 
 PV_STAGES = ("keys", "prep", "table", "msm", "encode")  # PV_STAGE_* order
 PV_PATH_AUTO, PV_PATH_STRAUS, PV_PATH_COMB = 0, 1, 2
+PATH_NAMES = ("straus", "comb")  # forced arithmetic paths (tests run every one)
 
 # exported symbol -> (restype, argtypes); kept in sync with include/plenum_verify.h
 _c_u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -65,6 +66,9 @@ SIGNATURES = {
     "pv_memcpy_h2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "pv_memcpy_d2h": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "pv_sync": (ctypes.c_int, []),
+    "pv_stream_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+    "pv_stream_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "pv_stream_sync": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 

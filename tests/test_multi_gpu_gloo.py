@@ -97,3 +97,40 @@ def test_shard_bounds_cover_and_align():
             verd = np.arange(n) % 3 == 0
             rows = [pack_words(verd[a:b].astype(np.uint8), wpr) for a, b in spans]
             assert np.array_equal(assemble(np.stack(rows) if rows else np.zeros((world, 0)), n, world), verd)
+
+
+def test_sharded_world8_gloo():
+    """The 8-rank split of configs[4] in miniature: 8 gloo ranks, one all-gather, every rank ends with
+    the single-process verdicts."""
+    test_sharded_verdicts_equal_single_process(8, 600)
+
+
+def test_config5_shard_arithmetic():
+    """bench.py's N > 1 default is configs[4]: 64M requests over N GPUs, i.e. ceil(64M / N) per GPU
+    in 64-aligned contiguous shards (8M per rank at N = 8, 8 launch chunks of 2^20), and the
+    shards tile the 64M batch exactly as plenum_amd.sharding splits it."""
+    import bench
+    total = bench.CONFIG5_TOTAL
+    assert total == 64 * 2 ** 20
+    for world in (2, 4, 8):
+        per = (total + world * 64 - 1) // (world * 64) * 64
+        spans = [shard_bounds(total, world, r) for r in range(world)]
+        assert all(hi - lo == per for lo, hi in spans), (world, spans[:2])
+        assert spans[-1][1] == total and words_per_rank(total, world) * 64 == per
+    assert (total // 8) == 8 * 2 ** 20 and (total // 8) // 2 ** 20 == 8
+
+
+def test_bench_expected_bits_match_tamper():
+    """The headline's must-reject records: every rank (re)computes each shard's expected bitmap from
+    the seed alone, and it equals the set adversarial_batch.tamper() corrupted."""
+    import bench
+    import adversarial_batch
+    n = 5000
+    blob = np.zeros(n * 100, np.uint8)
+    off = np.arange(0, n * 100 + 1, 100, dtype=np.uint64)
+    for rank in (0, 3, 7):
+        b2, idx = adversarial_batch.tamper(blob, off, bench.tamper_count(n), seed=1000 + rank)
+        want = bench.expected_bits(n, rank)
+        assert np.array_equal(np.nonzero(~want)[0], idx)
+        changed = np.nonzero((b2 != blob).reshape(n, 100).any(axis=1))[0]
+        assert np.array_equal(changed, idx)

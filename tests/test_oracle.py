@@ -60,3 +60,43 @@ def test_base58_reference_kat():
         b58decode("10")
     for data in (b"", b"\0", b"\0\0ab", bytes(range(40))):
         assert b58decode(b58encode(data).decode()) == data
+
+
+def test_sodium_forger_matches_oracle(oracle, sodium):
+    """bench.py builds configs[2] with tools/adversarial_batch.SodiumForger (libsodium's group API);
+    the tests use the C oracle's raw signer: same keys and signatures for the same scalars."""
+    import numpy as np
+    from adversarial_batch import ORDER8, SodiumForger
+    f = SodiumForger()
+    rng = np.random.default_rng(9)
+    L = 2 ** 252 + 27742317777372353535851937790883648493
+    for _ in range(20):
+        a = (int(rng.integers(1, 2 ** 62)) * int(rng.integers(1, 2 ** 62)) % L).to_bytes(32, "little")
+        r = (int(rng.integers(1, 2 ** 62)) * 7919 % L).to_bytes(32, "little")
+        A = f.scalarmult_base(a)
+        assert A == oracle.scalarmult_base(a)
+        A2 = f.point_add(A, ORDER8)
+        assert A2 == oracle.point_add(A, ORDER8)
+        m = rng.bytes(int(rng.integers(0, 300)))
+        s = f.sign_raw(r, a, A2, m)
+        assert s == oracle.sign_raw(r, a, A2, m)
+        assert sodium.sign_open_ok(s + m, A2) == oracle.sign_open_ok(s + m, A2)
+
+
+def test_config3_batch_with_sodium_forger(oracle):
+    """configs[2] as bench.py builds it (libsodium forger), small: untouched records valid, mutated
+    ones rejected except mixed-order keys whose k happens to be a multiple of 8."""
+    import numpy as np
+    import nym_workload
+    from adversarial_batch import inject
+    from oracle.oracle import cpu_verdicts
+    blob, off, pks = nym_workload.generate(0, 3000, workers=1)
+    blob2, pks2, idx, labels = inject(blob, off, pks, 0.05, seed=3)
+    got = cpu_verdicts(blob2, off, pks2)
+    mask = np.ones(len(got), bool)
+    mask[idx] = False
+    assert got[mask].all()
+    lab = np.array(labels)
+    assert not got[idx[lab != "mixed_order_A"]].any()
+    o = np.array([oracle.sign_open_ok(blob2[off[i]:off[i + 1]].tobytes(), pks2[i].tobytes()) for i in idx])
+    assert np.array_equal(o, got[idx])
