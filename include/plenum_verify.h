@@ -102,7 +102,13 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
  *   PV_PATH_COMB    per batch: deduplicate keys; per DISTINCT key: decompress and expand a
  *                   radix-256 comb table; per request: 48 table additions, no doublings (keys
  *                   beyond the PV_KEY_CAP = 16,384 tables a chunk holds take the Straus path)
- *   PV_PATH_AUTO    (default) per chunk of >= 32,768 requests: deduplicate keys, give a comb table
+ *   PV_PATH_LATENCY per request: one workgroup (two waves) with limb-parallel arithmetic, every
+ *                   field element spread over 10 lanes of a 16-lane row; decompression of A and R in
+ *                   one chain, [S]B from the fixed-base comb, [k](-A) by 252 doublings + 64
+ *                   additions, and the comparison with R without an inversion. One kernel launch;
+ *                   the fastest path for small batches (Plenum's 100 / 1,000-message quotas)
+ *   PV_PATH_AUTO    (default) batches of <= 2,048 requests take the latency path; otherwise
+ *                   per chunk of >= 32,768 requests: deduplicate keys, give a comb table
  *                   to every key with >= 48 requests in the chunk (a table costs about what ~50
  *                   requests save) and verify the other requests on the Straus path in the same
  *                   launch; smaller chunks go Straus. Split on the device, so
@@ -111,6 +117,7 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
 #define PV_PATH_AUTO 0
 #define PV_PATH_STRAUS 1
 #define PV_PATH_COMB 2
+#define PV_PATH_LATENCY 3
 int pv_set_path(int mode);
 /* The path the most recent chunk took (PV_PATH_COMB if any of its requests used a comb table, else
  * PV_PATH_STRAUS) and its distinct-key count (0 when no key kernels ran). Synchronises the device. */

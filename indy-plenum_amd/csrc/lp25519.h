@@ -1,0 +1,555 @@
+// Limb-parallel ("lp") GF(2^255-19) and Edwards25519 arithmetic for the low-latency path.
+//
+// The throughput kernels keep one verification per lane, so one verification is a long serial
+// instruction stream: at Plenum's real batch sizes (a ZStack quota is 100 client / 1,000 node
+// messages, stp_core/config.py:32-33) the GPU is nearly idle and that stream's length IS the
+// latency. Here ONE wave works on ONE verification and spreads every field element over the lanes:
+//
+//   a field element lives in one 16-lane DPP row, lane k (k = 0..9) holding limb k of the radix-2^25.5
+//   representation of fe25519.h (lanes 10..15 are scratch); the wave's four rows hold four elements,
+//   e.g. the four coordinates of a point, or the four products of one group operation.
+//
+// A product h = f g is computed by every lane for its own column k, row by row in parallel:
+//   h_k = sum_i  f_i * g_{(k - i) mod 10} * (19 if k < i) * (2 if i and k - i are odd)
+// with f_i broadcast inside the row (DPP row_newbcast:i) and g rotated (DPP row_ror:i) from an
+// "extended" copy whose scratch lanes 10..15 already hold 19 g_4 .. 19 g_9 (so most wrapped terms
+// need no select); the column sums are then carried across lanes with two DPP shift passes.
+// Rows are exchanged with gfx950's v_permlane16_swap / v_permlane32_swap (three instructions give
+// every row all four rows). One lp multiplication is ~70 wave instructions (10 v_mad_u64_u32)
+// instead of ~160 (100 mads) for a per-lane fe_mul, and four of them run at once, so a point
+// doubling takes two multiplication latencies.
+//
+// The same source compiles for the host with lu/lu64/lm = 64-lane arrays and the cross-lane
+// operations simulated exactly (tests/native/hostcheck.hip, tests/test_native_host.py), with the
+// limb bounds asserted under PV_BOUNDS_CHECK. Bound names: "LR" = limb < 2^w + 2^22.6 (w = 26 even,
+// 25 odd), the output of lp_mul; lp_mul needs g limbs < 2^27.75 (19 g < 2^32), f limbs < 2^31, and
+// every column < 2^64 (checked on the host).
+#pragma once
+#include "fe25519.h"
+#include "ge25519.h"
+#include "comb.h"
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define LP_DEVICE 1
+#else
+#define LP_DEVICE 0
+#endif
+
+// ------------------------------------------------------------------ lane vectors
+#if LP_DEVICE
+typedef uint32_t lu;    // this lane's 32-bit value
+typedef uint64_t lu64;  // this lane's 64-bit value
+typedef bool lm;        // this lane's predicate
+#define LP_FN __device__ __forceinline__
+
+LP_FN lu lp_lane() { return __lane_id(); }
+LP_FN lu lp_sel(lm c, lu a, lu b) { return c ? a : b; }
+LP_FN lu64 lp_sel64(lm c, lu64 a, lu64 b) { return c ? a : b; }
+LP_FN lm lp_and(lm a, lm b) { return a && b; }
+LP_FN lm lp_lt(lu a, uint32_t b) { return a < b; }
+LP_FN lm lp_le(lu a, uint32_t b) { return a <= b; }
+LP_FN lm lp_ge(lu a, uint32_t b) { return a >= b; }
+LP_FN lm lp_eq(lu a, uint32_t b) { return a == b; }
+LP_FN lu lp_lo(lu64 x) { return (uint32_t)x; }
+LP_FN lu lp_hi(lu64 x) { return (uint32_t)(x >> 32); }
+LP_FN lu64 lp_wide(lu x) { return (uint64_t)x; }
+LP_FN lu64 lp_join(lu hi, lu lo) { return ((uint64_t)hi << 32) | lo; }
+LP_FN lu64 lp_shr64(lu64 x, lu s) { return x >> s; }
+LP_FN lu lp_shrv(lu x, lu s) { return x >> s; }
+// 64-bit multiply-accumulate: one v_mad_u64_u32
+LP_FN lu64 lp_mad(lu a, lu b, lu64 c) { return (uint64_t)a * b + c; }
+// DPP row operations (row = 16 lanes): lanes whose source is outside the row read 0
+template <int CTRL>
+LP_FN lu lp_dpp(lu x) { return (lu)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true); }
+template <int I> LP_FN lu lp_bcast(lu x) { return lp_dpp<0x150 + I>(x); }  // row_newbcast:I
+template <int I> LP_FN lu lp_ror(lu x) { return I == 0 ? x : lp_dpp<0x120 + I>(x); }  // row_ror:I
+template <int I> LP_FN lu lp_shr(lu x) { return lp_dpp<0x110 + I>(x); }  // row_shr:I (lane k <- k - I)
+template <int I> LP_FN lu lp_shl(lu x) { return lp_dpp<0x100 + I>(x); }  // row_shl:I (lane k <- k + I)
+// gfx950 row exchange: (a, b) -> a with its odd rows replaced by b's even rows, b with its even rows
+// replaced by a's odd rows (permlane16); the same on 32-lane halves (permlane32)
+LP_FN void lp_swap16(lu& a, lu& b) {
+    auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+}
+LP_FN void lp_swap32(lu& a, lu& b) {
+    auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0];
+    b = r[1];
+}
+LP_FN uint32_t lp_readlane(lu x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+LP_FN lu lp_gather(const uint32_t* base, lu idx) { return base[idx]; }
+#define LP_CHECK(cond, msg) do { } while (0)
+
+#else  // ---------------------------------------------------------- host simulation (64 lanes)
+#include <stdio.h>
+#include <stdlib.h>
+#define LP_FN inline
+struct lu {
+    uint32_t v[64];
+    lu() {}
+    lu(uint32_t c) { for (int l = 0; l < 64; l++) v[l] = c; }
+};
+struct lu64 {
+    uint64_t v[64];
+    lu64() {}
+    lu64(uint64_t c) { for (int l = 0; l < 64; l++) v[l] = c; }
+};
+struct lm {
+    bool v[64];
+};
+#define LP_MAP(T, expr) T r; for (int l = 0; l < 64; l++) r.v[l] = (expr); return r
+LP_FN lu operator+(const lu& a, const lu& b) { LP_MAP(lu, a.v[l] + b.v[l]); }
+LP_FN lu operator-(const lu& a, const lu& b) { LP_MAP(lu, a.v[l] - b.v[l]); }
+LP_FN lu operator*(const lu& a, const lu& b) { LP_MAP(lu, a.v[l] * b.v[l]); }
+LP_FN lu operator&(const lu& a, const lu& b) { LP_MAP(lu, a.v[l] & b.v[l]); }
+LP_FN lu operator|(const lu& a, const lu& b) { LP_MAP(lu, a.v[l] | b.v[l]); }
+LP_FN lu operator^(const lu& a, const lu& b) { LP_MAP(lu, a.v[l] ^ b.v[l]); }
+LP_FN lu operator>>(const lu& a, int s) { LP_MAP(lu, a.v[l] >> s); }
+LP_FN lu operator<<(const lu& a, int s) { LP_MAP(lu, a.v[l] << s); }
+LP_FN lu64 operator+(const lu64& a, const lu64& b) { LP_MAP(lu64, a.v[l] + b.v[l]); }
+LP_FN lu64 operator>>(const lu64& a, int s) { LP_MAP(lu64, a.v[l] >> s); }
+LP_FN lu64 operator<<(const lu64& a, int s) { LP_MAP(lu64, a.v[l] << s); }
+LP_FN lu lp_lane() { LP_MAP(lu, (uint32_t)l); }
+LP_FN lu lp_sel(const lm& c, const lu& a, const lu& b) { LP_MAP(lu, c.v[l] ? a.v[l] : b.v[l]); }
+LP_FN lu64 lp_sel64(const lm& c, const lu64& a, const lu64& b) { LP_MAP(lu64, c.v[l] ? a.v[l] : b.v[l]); }
+LP_FN lm lp_and(const lm& a, const lm& b) { LP_MAP(lm, a.v[l] && b.v[l]); }
+LP_FN lm lp_lt(const lu& a, uint32_t b) { LP_MAP(lm, a.v[l] < b); }
+LP_FN lm lp_le(const lu& a, uint32_t b) { LP_MAP(lm, a.v[l] <= b); }
+LP_FN lm lp_ge(const lu& a, uint32_t b) { LP_MAP(lm, a.v[l] >= b); }
+LP_FN lm lp_eq(const lu& a, uint32_t b) { LP_MAP(lm, a.v[l] == b); }
+LP_FN lu lp_lo(const lu64& x) { LP_MAP(lu, (uint32_t)x.v[l]); }
+LP_FN lu lp_hi(const lu64& x) { LP_MAP(lu, (uint32_t)(x.v[l] >> 32)); }
+LP_FN lu64 lp_wide(const lu& x) { LP_MAP(lu64, (uint64_t)x.v[l]); }
+LP_FN lu64 lp_join(const lu& hi, const lu& lo) { LP_MAP(lu64, ((uint64_t)hi.v[l] << 32) | lo.v[l]); }
+LP_FN lu64 lp_shr64(const lu64& x, const lu& s) { LP_MAP(lu64, x.v[l] >> s.v[l]); }
+LP_FN lu lp_shrv(const lu& x, const lu& s) { LP_MAP(lu, x.v[l] >> s.v[l]); }
+LP_FN lu64 lp_mad(const lu& a, const lu& b, const lu64& c) {
+    LP_MAP(lu64, (uint64_t)a.v[l] * b.v[l] + c.v[l]);
+}
+template <int I> LP_FN lu lp_bcast(const lu& x) { LP_MAP(lu, x.v[(l & ~15) + I]); }
+template <int I> LP_FN lu lp_ror(const lu& x) { LP_MAP(lu, x.v[(l & ~15) + (((l & 15) - I) & 15)]); }
+template <int I> LP_FN lu lp_shr(const lu& x) { LP_MAP(lu, (l & 15) >= I ? x.v[l - I] : 0u); }
+template <int I> LP_FN lu lp_shl(const lu& x) { LP_MAP(lu, (l & 15) + I < 16 ? x.v[l + I] : 0u); }
+LP_FN void lp_swap16(lu& a, lu& b) {
+    lu na = a, nb = b;
+    for (int l = 0; l < 64; l++) {
+        const int row = l >> 4;
+        if (row & 1) na.v[l] = b.v[l - 16];   // a's odd rows <- b's even rows
+        else nb.v[l] = a.v[l + 16];           // b's even rows <- a's odd rows
+    }
+    a = na;
+    b = nb;
+}
+LP_FN void lp_swap32(lu& a, lu& b) {
+    lu na = a, nb = b;
+    for (int l = 0; l < 32; l++) {
+        na.v[l + 32] = b.v[l];  // a's upper half <- b's lower half
+        nb.v[l] = a.v[l + 32];  // b's lower half <- a's upper half
+    }
+    a = na;
+    b = nb;
+}
+LP_FN uint32_t lp_readlane(const lu& x, int l) { return x.v[l]; }
+LP_FN lu lp_gather(const uint32_t* base, const lu& idx) { LP_MAP(lu, base[idx.v[l]]); }
+#undef LP_MAP
+#ifdef PV_BOUNDS_CHECK
+#define LP_CHECK(cond, msg) do { if (!(cond)) { fprintf(stderr, "lp bound violated: %s\n", msg); abort(); } } while (0)
+#else
+#define LP_CHECK(cond, msg) do { } while (0)
+#endif
+#endif  // LP_DEVICE
+
+#if !LP_DEVICE
+// host bound checks on the limb lanes (k < 10) only
+inline void lp_check_limbs(const lu& x, uint32_t bound, const char* msg) {
+#ifdef PV_BOUNDS_CHECK
+    for (int l = 0; l < 64; l++)
+        if ((l & 15) < 10) LP_CHECK(x.v[l] < bound, msg);
+#else
+    (void)x; (void)bound; (void)msg;
+#endif
+}
+#define LP_BOUND(x, b, msg) lp_check_limbs(x, b, msg)
+#else
+#define LP_BOUND(x, b, msg) do { } while (0)
+#endif
+
+// ------------------------------------------------------------------ per-lane constants
+struct LpLane {
+    lu k;        // limb index within the row (lane & 15)
+    lu row;      // row index (lane >> 4)
+    lu w;        // limb width: 26 (even k) / 25 (odd k)
+    lu mask;     // 2^w - 1
+    lu two_p;    // limb k of 2p (fe_sub's offset)
+    lu four_p;   // limb k of 4p
+    lm k0;       // k == 0
+    lm kge10;    // scratch lane
+    lm keven;
+    lm row0, row1, row2, row3;
+    LP_FN static LpLane make() {
+        LpLane c;
+        const lu lane = lp_lane();
+        c.k = lane & 15u;
+        c.row = lane >> 4;
+        const lm odd = lp_eq(c.k & 1u, 1u);
+        c.w = lp_sel(odd, 25u, 26u);
+        c.mask = lp_sel(odd, (uint32_t)M25, (uint32_t)M26);
+        c.k0 = lp_eq(c.k, 0u);
+        c.two_p = lp_sel(c.k0, 0x7FFFFDAu, lp_sel(odd, 0x3FFFFFEu, 0x7FFFFFEu));
+        c.four_p = lp_sel(c.k0, 0xFFFFFB4u, lp_sel(odd, 0x7FFFFFCu, 0xFFFFFFCu));
+        c.kge10 = lp_ge(c.k, 10u);
+        c.keven = lp_eq(c.k & 1u, 0u);
+        c.row0 = lp_eq(c.row, 0u);
+        c.row1 = lp_eq(c.row, 1u);
+        c.row2 = lp_eq(c.row, 2u);
+        c.row3 = lp_eq(c.row, 3u);
+        return c;
+    }
+    // limb k of a constant fe (same value in every row)
+    LP_FN lu limb(const uint32_t c[10]) const {
+        lu r = 0u;
+#pragma unroll
+        for (int i = 0; i < 10; i++) r = lp_sel(lp_eq(k, (uint32_t)i), c[i], r);
+        return r;
+    }
+    // row r of the result from a, b, c, d
+    LP_FN lu rows(const lu& a, const lu& b, const lu& c, const lu& d) const {
+        return lp_sel(row0, a, lp_sel(row1, b, lp_sel(row2, c, d)));
+    }
+};
+
+// ------------------------------------------------------------------ field operations
+LP_FN lu lp_add(const lu& a, const lu& b) { return a + b; }
+// a + 2p - b (b limbs <= 2p limbs, e.g. LR)
+LP_FN lu lp_sub(const LpLane& c, const lu& a, const lu& b) { return a + c.two_p - b; }
+LP_FN lu lp_sub4p(const LpLane& c, const lu& a, const lu& b) { return a + c.four_p - b; }
+
+// One 32-bit carry pass: limbs < 2^32 - 2^13 -> limb < 2^w + 19 * 2^7 (the wrap goes to limb 0).
+LP_FN lu lp_carry1(const LpLane& c, const lu& x) {
+    const lu cy = lp_shrv(x, c.w);
+    const lu l = x & c.mask;
+    const lu in = lp_sel(c.k0, lp_shl<9>(cy) * 19u, lp_shr<1>(cy));
+    return l + in;
+}
+
+// h = f g (row by row). f limbs < 2^31, g limbs < 2^27.75; output LR.
+LP_FN lu lp_mul(const LpLane& c, const lu& f, const lu& g) {
+    LP_BOUND(g, 0xD800000u, "lp_mul g operand");
+    LP_BOUND(f, 0x80000000u, "lp_mul f operand");
+    // g extended: lanes m >= 6 of Y hold 19 g_{m-6}; X = g on lanes 0..9, Y on scratch lanes 10..15
+    const lu Y = lp_shr<6>(g) * 19u;
+    const lu X = lp_sel(c.kge10, Y, g);
+    const lu f2 = f + f;
+    lu64 acc = lp_mad(lp_bcast<0>(f), X, lu64(0ull));
+#define LP_TERM(I)                                                                        \
+    {                                                                                     \
+        lu fi = lp_bcast<I>(f);                                                           \
+        if (I & 1) fi = lp_sel(c.keven, lp_bcast<I>(f2), fi);                             \
+        lu gi = lp_ror<I>(X);                                                             \
+        if (I >= 7) gi = lp_sel(lp_le(c.k, (uint32_t)(I - 7)), lp_ror<I>(Y), gi);         \
+        acc = lp_mad(fi, gi, acc);                                                        \
+    }
+    LP_TERM(1) LP_TERM(2) LP_TERM(3) LP_TERM(4) LP_TERM(5) LP_TERM(6) LP_TERM(7) LP_TERM(8) LP_TERM(9)
+#undef LP_TERM
+#if !LP_DEVICE && defined(PV_BOUNDS_CHECK)
+    {   // exact column bound: recompute each lane's column in 128 bits
+        for (int l = 0; l < 64; l++) {
+            const int k = l & 15, base = l & ~15;
+            if (k >= 10) continue;
+            unsigned __int128 s = 0;
+            for (int i = 0; i < 10; i++) {
+                const int j = ((k - i) % 10 + 10) % 10;
+                unsigned __int128 t = (unsigned __int128)f.v[base + i] * g.v[base + j];
+                if (k < i) t *= 19;
+                if ((i & 1) && (j & 1)) t *= 2;
+                s += t;
+            }
+            LP_CHECK((s >> 64) == 0, "lp_mul column overflow");
+            LP_CHECK((uint64_t)s == acc.v[l], "lp_mul column mismatch");
+        }
+    }
+#endif
+    // carry pass 1 (64-bit): column k -> limb k + carry from k - 1 (19 * carry of 9 into limb 0)
+    const lu64 cy = lp_shr64(acc, c.w);
+    const lu lo = lp_lo(acc) & c.mask;
+    const lu clo = lp_lo(cy), chi = lp_hi(cy);  // cy < 2^39
+    const lu wlo = lp_shl<9>(clo), whi = lp_shl<9>(chi);
+    const lu64 w19 = lp_mad(wlo, 19u, lp_join(whi * 19u, 0u));
+    const lu64 in = lp_sel64(c.k0, w19, lp_join(lp_shr<1>(chi), lp_shr<1>(clo)));
+    const lu64 t = in + lp_wide(lo);  // < 2^26 + 2^43.3
+    // carry pass 2 (32-bit)
+    const lu cy2 = lp_lo(lp_shr64(t, c.w));  // < 2^18.3
+    const lu l2 = lp_lo(t) & c.mask;
+    const lu h = l2 + lp_sel(c.k0, lp_shl<9>(cy2) * 19u, lp_shr<1>(cy2));
+    LP_BOUND(h, (1u << 26) + (1u << 23), "lp_mul output");
+    return h;
+}
+LP_FN lu lp_sq(const LpLane& c, const lu& f) { return lp_mul(c, f, f); }
+
+// every row gets row r of x: o0 = row 0 in all rows, ... (3 permlane instructions)
+LP_FN void lp_allrows(const lu& x, lu& o0, lu& o1, lu& o2, lu& o3) {
+    lu p = x, q = x;
+    lp_swap16(p, q);  // p = [x0 x0 x2 x2], q = [x1 x1 x3 x3]
+    o0 = p;
+    o2 = p;
+    lp_swap32(o0, o2);  // o0 = [x0 x0 x0 x0], o2 = [x2 x2 x2 x2]
+    o1 = q;
+    o3 = q;
+    lp_swap32(o1, o3);
+}
+
+// z^(2^252 - 3) in every row at once (libsodium's chain, as fe_pow22523)
+LP_FN lu lp_sqn(const LpLane& c, lu x, int n) {
+    for (int i = 0; i < n; i++) x = lp_sq(c, x);
+    return x;
+}
+LP_FN lu lp_pow22523(const LpLane& c, const lu& z) {
+    lu t0 = lp_sq(c, z);                 // z^2
+    lu t1 = lp_sqn(c, t0, 2);            // z^8
+    t1 = lp_mul(c, z, t1);               // z^9
+    t0 = lp_mul(c, t0, t1);              // z^11
+    lu t2 = lp_sq(c, t0);                // z^22
+    t1 = lp_mul(c, t1, t2);              // z^(2^5 - 1)
+    t2 = lp_sqn(c, t1, 5);
+    t1 = lp_mul(c, t2, t1);              // z^(2^10 - 1)
+    t2 = lp_sqn(c, t1, 10);
+    t2 = lp_mul(c, t2, t1);              // z^(2^20 - 1)
+    lu t3 = lp_sqn(c, t2, 20);
+    t2 = lp_mul(c, t3, t2);              // z^(2^40 - 1)
+    t2 = lp_sqn(c, t2, 10);
+    t1 = lp_mul(c, t2, t1);              // z^(2^50 - 1)
+    t2 = lp_sqn(c, t1, 50);
+    t2 = lp_mul(c, t2, t1);              // z^(2^100 - 1)
+    t3 = lp_sqn(c, t2, 100);
+    t2 = lp_mul(c, t3, t2);              // z^(2^200 - 1)
+    t2 = lp_sqn(c, t2, 50);
+    t1 = lp_mul(c, t2, t1);              // z^(2^250 - 1)
+    t1 = lp_sqn(c, t1, 2);               // z^(2^252 - 4)
+    return lp_mul(c, t1, z);             // z^(2^252 - 3)
+}
+
+// The 10 limbs of row r as a scalar fe (uniform values: v_readlane).
+LP_FN fe lp_row_fe(const lu& x, int r) {
+    fe h;
+#pragma unroll
+    for (int i = 0; i < 10; i++) h.v[i] = lp_readlane(x, 16 * r + i);
+    return h;
+}
+
+// Lane k of the row gets limb k of the 255-bit little-endian value s[8] (bit 255 ignored), as
+// fe_frombytes32. s may differ per row (each lane passes its own row's words).
+LP_FN lu lp_from_words(const LpLane& c, const lu s[8]) {
+    // limb k = bits [o_k, o_k + w_k) with o = 0, 26, 51, 77, 102, 128, 153, 179, 204, 230
+    lu r = 0u;
+#define LP_LIMB(K, EXPR) r = lp_sel(lp_eq(c.k, (uint32_t)(K)), (EXPR), r)
+    LP_LIMB(0, s[0] & M26);
+    LP_LIMB(1, ((s[0] >> 26) | (s[1] << 6)) & M25);
+    LP_LIMB(2, ((s[1] >> 19) | (s[2] << 13)) & M26);
+    LP_LIMB(3, ((s[2] >> 13) | (s[3] << 19)) & M25);
+    LP_LIMB(4, (s[3] >> 6) & M26);
+    LP_LIMB(5, s[4] & M25);
+    LP_LIMB(6, ((s[4] >> 25) | (s[5] << 7)) & M26);
+    LP_LIMB(7, ((s[5] >> 19) | (s[6] << 13)) & M25);
+    LP_LIMB(8, ((s[6] >> 12) | (s[7] << 20)) & M26);
+    LP_LIMB(9, (s[7] >> 6) & M25);
+#undef LP_LIMB
+    return r;
+}
+
+// ------------------------------------------------------------------ group operations
+// Layouts (one lu, rows 0..3):
+//   ext      [X, Y, Z, T]          extended coordinates (p3), every limb LR
+//   cached   [Y-X, Y+X, 2dT, 2Z]   addend; an affine niels entry [y-x, y+x, 2dxy, 2] has the same form
+// Addition / doubling end with a p1p1 -> p3 multiplication, so every result is a full ext point.
+
+// r = p + q (q cached or niels, possibly negated by the caller)
+LP_FN lu lp_add_cached(const LpLane& c, const lu& p, const lu& q) {
+    lu X, Y, Z, T;
+    lp_allrows(p, X, Y, Z, T);
+    const lu f = c.rows(lp_sub(c, Y, X), Y + X, T, Z);  // (Y-X, Y+X, T, Z): < 2^27.6
+    const lu abcd = lp_mul(c, f, q);                     // [A, B, C, D]
+    lu A, B, C, D;
+    lp_allrows(abcd, A, B, C, D);
+    const lu E = lp_sub(c, B, A), H = B + A, G = D + C, F = lp_sub(c, D, C);
+    // X3 = E F, Y3 = G H, Z3 = F G, T3 = E H
+    return lp_mul(c, c.rows(E, G, F, E), c.rows(F, H, G, H));
+}
+
+// r = 2 p (dbl-2008-hwcd: XX, YY, ZZ, (X+Y)^2 in the four rows at once)
+LP_FN lu lp_dbl(const LpLane& c, const lu& p) {
+    lu X, Y, Z, T;
+    lp_allrows(p, X, Y, Z, T);
+    const lu sq = lp_sq(c, c.rows(X, Y, Z, X + Y));  // [XX, YY, ZZ, SS]
+    lu XX, YY, ZZ, SS;
+    lp_allrows(sq, XX, YY, ZZ, SS);
+    const lu rY = YY + XX;                            // H
+    const lu rZ = lp_sub(c, YY, XX);                  // G
+    const lu rX = lp_sub4p(c, SS, rY);                // E, < 2^28.4: f side only
+    const lu rT = lp_carry1(c, lp_sub4p(c, ZZ + ZZ, rZ));  // F (carried: a g operand)
+    // X3 = E F, Y3 = H G, Z3 = G F, T3 = E H
+    return lp_mul(c, c.rows(rX, rY, rZ, rX), c.rows(rT, rZ, rT, rY));
+}
+
+// ext -> cached [Y-X, Y+X, 2dT, 2Z] (one multiplication: every component reduced)
+LP_FN lu lp_to_cached(const LpLane& c, const lu& p, const lu& d2) {
+    lu X, Y, Z, T;
+    lp_allrows(p, X, Y, Z, T);
+    const lu one = lp_sel(c.k0, 1u, 0u), two = lp_sel(c.k0, 2u, 0u);
+    return lp_mul(c, c.rows(lp_sub(c, Y, X), Y + X, T, Z), c.rows(one, one, d2, two));
+}
+
+// -q for a cached / niels addend: swap rows 0 and 1, negate row 2
+LP_FN lu lp_neg_cached(const LpLane& c, const lu& q) {
+    lu p = q, s = q;
+    lp_swap16(p, s);  // p = [q0 q0 q2 q2], s = [q1 q1 q3 q3]
+    return c.rows(s, p, lp_sub(c, 0u, q), q);
+}
+
+LP_FN lu lp_identity_ext(const LpLane& c) {
+    const lu one = lp_sel(c.k0, 1u, 0u);
+    return c.rows(0u, one, one, 0u);
+}
+
+// ------------------------------------------------------------------ verification pieces
+// Constants every lp routine needs, one VGPR each (limb k of the row).
+struct LpConsts {
+    lu d, d2, sqrtm1, one;
+    LP_FN static LpConsts make(const LpLane& c) {
+        LpConsts k;
+        k.d = c.limb(PV_D);
+        k.d2 = c.limb(PV_D2);
+        k.sqrtm1 = c.limb(PV_SQRTM1);
+        k.one = lp_sel(c.k0, 1u, 0u);
+        return k;
+    }
+};
+
+// Canonical-zero / parity tests of one row (uniform: the row's limbs are read into scalars).
+LP_FN bool lp_row_iszero(const lu& x, int r) { return fe_iszero(lp_row_fe(x, r)); }
+LP_FN uint32_t lp_row_isnegative(const lu& x, int r) { return fe_isnegative(lp_row_fe(x, r)); }
+
+// Decompression of the key A (row 0, returned negated: -A, as ge_frombytes_negate) and of the
+// signature's R (row 1, NOT negated: x with parity = R's bit 255), both in one pass of the
+// x^((p-5)/8) chain. s[8] = this lane's row's encoding (A's words in row 0, R's in row 1; rows 2-3
+// repeat them). Outputs: X, Y with the x / y of row 0 (-A) and row 1 (R); ok_a / ok_r = the point
+// decompresses ((y^2-1)/(dy^2+1) is a square); x_r_zero = R's x is 0.
+struct LpDecomp {
+    lu X, Y;
+    bool ok_a, ok_r, x_r_zero;
+};
+LP_FN LpDecomp lp_decompress_ar(const LpLane& c, const LpConsts& K, const lu s[8]) {
+    LpDecomp o;
+    const lu y = lp_from_words(c, s);
+    lu u = lp_sq(c, y);
+    lu v = lp_mul(c, u, K.d);
+    u = lp_carry1(c, lp_sub(c, u, K.one));  // u = y^2 - 1
+    v = lp_carry1(c, v + K.one);              // v = d y^2 + 1
+    lu v3 = lp_mul(c, lp_sq(c, v), v);        // v^3
+    lu x = lp_mul(c, lp_mul(c, lp_sq(c, v3), v), u);  // u v^7
+    x = lp_pow22523(c, x);
+    x = lp_mul(c, lp_mul(c, x, v3), u);       // u v^3 (u v^7)^((p-5)/8)
+    const lu vxx = lp_mul(c, lp_sq(c, x), v);
+    const lu chk_m = lp_sub(c, vxx, u), chk_p = vxx + u;
+    const bool ok0 = lp_row_iszero(chk_m, 0), ok1 = lp_row_iszero(chk_m, 1);
+    o.ok_a = ok0 || lp_row_iszero(chk_p, 0);
+    o.ok_r = ok1 || lp_row_iszero(chk_p, 1);
+    const lu xs = lp_mul(c, x, K.sqrtm1);
+    // per row: x or x sqrt(-1)
+    const lm use_s = lp_and(lp_lt(c.row, 2u), lp_eq(lp_sel(c.row0, ok0 ? 0u : 1u, ok1 ? 0u : 1u), 1u));
+    x = lp_sel(use_s, xs, x);
+    // sign: row 0 (A) negated iff parity == sign bit (ge_frombytes_negate); row 1 (R) iff parity != sign
+    const uint32_t sa = lp_readlane(s[7], 0) >> 31, sr = lp_readlane(s[7], 16) >> 31;
+    const uint32_t pa = lp_row_isnegative(x, 0), pr = lp_row_isnegative(x, 1);
+    o.x_r_zero = lp_row_iszero(x, 1);
+    const uint32_t neg0 = pa == sa ? 1u : 0u, neg1 = pr != sr ? 1u : 0u;
+    const lm neg = lp_eq(lp_sel(c.row0, neg0, lp_sel(c.row1, neg1, 0u)), 1u);
+    o.X = lp_sel(neg, lp_carry1(c, lp_sub(c, 0u, x)), x);
+    o.Y = y;
+    return o;
+}
+
+// ext point from row `r` of X and Y (Z = 1, T = X Y): the decompressed key as [X, Y, Z, T]
+LP_FN lu lp_ext_from_xy(const LpLane& c, const LpConsts& K, const lu& X, const lu& Y, int r) {
+    lu xr[4], yr[4];
+    lp_allrows(X, xr[0], xr[1], xr[2], xr[3]);
+    lp_allrows(Y, yr[0], yr[1], yr[2], yr[3]);
+    const lu x = r == 0 ? xr[0] : xr[1], y = r == 0 ? yr[0] : yr[1];
+    // rows [X, Y, 1, X Y]: one multiplication forms T (rows 0-2 multiply by 1)
+    return lp_mul(c, c.rows(x, y, K.one, x), c.rows(K.one, K.one, K.one, y));
+}
+
+// The table of [j](-A), j = -8..8, cached form, for the signed radix-16 digits of k. store(j, q).
+template <class Store>
+LP_FN void lp_build_a_table(const LpLane& c, const LpConsts& K, const lu& negA, const Store& store) {
+    const lu one = K.one, two = lp_sel(c.k0, 2u, 0u);
+    store(0, c.rows(one, one, 0u, two));  // identity
+    const lu c1 = lp_to_cached(c, negA, K.d2);
+    store(1, c1);
+    store(-1, lp_neg_cached(c, c1));
+    lu cur = lp_dbl(c, negA);
+    for (int j = 2; j <= 8; j++) {
+        if (j > 2) cur = lp_add_cached(c, cur, c1);
+        const lu cj = lp_to_cached(c, cur, K.d2);
+        store(j, cj);
+        store(-j, lp_neg_cached(c, cj));
+    }
+}
+
+// [k](-A) by regular signed radix-16 windows: 63 x 4 doublings + 64 table additions. digit(i) =
+// the i-th signed digit (wave-uniform), load(e) = the table entry for digit e.
+template <class Digit, class Load>
+LP_FN lu lp_straus_a(const LpLane& c, const Digit& digit, const Load& load) {
+    lu acc = lp_add_cached(c, lp_identity_ext(c), load(digit(63)));
+    for (int win = 62; win >= 0; win--) {
+        acc = lp_dbl(c, lp_dbl(c, lp_dbl(c, lp_dbl(c, acc))));
+        acc = lp_add_cached(c, acc, load(digit(win)));
+    }
+    return acc;
+}
+
+// Entry d = |f| of position j of the fixed-base comb T_B (comb.h: affine niels, words y+x at 0..9,
+// y-x at 10..19, 2dxy at 20..29 of a PV_BCOMB_STRIDE-word entry) in lp cached layout
+// [y-x, y+x, 2dxy, 2], negated for f < 0 (y+x <-> y-x, -2dxy).
+LP_FN lu lp_bcomb_entry(const LpLane& c, const uint32_t* bcomb, int j, int f) {
+    const bool neg = f < 0;
+    const uint32_t d = (uint32_t)(neg ? -f : f);
+    const uint32_t* e = bcomb + ((uint64_t)j * PV_BCOMB_ENT + d) * PV_BCOMB_STRIDE;
+    const lu kk = lp_sel(c.kge10, 9u, c.k);
+    const lu w = lp_sel(c.row0, neg ? kk : kk + 10u, lp_sel(c.row1, neg ? kk + 10u : kk, kk + 20u));
+    return lp_gather(e, w);
+}
+LP_FN lu lp_bcomb_fix(const LpLane& c, const lu& raw, int f) {
+    lu v = raw;
+    if (f < 0) v = lp_sel(c.row2, lp_sub(c, 0u, v), v);
+    return lp_sel(c.row3, lp_sel(c.k0, 2u, 0u), v);
+}
+
+// [S]B from the fixed-base comb T_B[j][|f_j|] (comb.h: 16 signed radix-65536 digits of S). entry(j)
+// returns the niels entry of position j for its digit, already in lp cached form (negated for a
+// negative digit): [y-x, y+x, 2dxy, 2].
+template <class Entry>
+LP_FN lu lp_comb_b(const LpLane& c, const Entry& entry) {
+    lu acc = lp_identity_ext(c);
+    for (int j = 15; j >= 0; j--) acc = lp_add_cached(c, acc, entry(j));
+    return acc;
+}
+
+// The final check: Q = QA + SB (SB as ext), then libsodium's encode(Q) == R rewritten without an
+// inversion: R canonical (checked by the caller), R decompressed (X row 1 = x_R with R's sign,
+// Y row 1 = y_R), and x_R != 0 or sign 0; accept iff X_Q = x_R Z_Q and Y_Q = y_R Z_Q. Given y_Q =
+// y_R, the two roots x, -x have opposite parity (p odd) unless x = 0, so parity(x_Q) = sign(R)
+// exactly when x_Q is the root decompression picked; y_Q = y_R < p is the canonical-y condition.
+LP_FN bool lp_final_check(const LpLane& c, const LpConsts& K, const lu& QA, const lu& SB, const lu& X, const lu& Y) {
+    const lu sb = lp_to_cached(c, SB, K.d2);
+    const lu Q = lp_add_cached(c, QA, sb);
+    lu QX, QY, QZ, QT;
+    lp_allrows(Q, QX, QY, QZ, QT);
+    lu xr[4], yr[4];
+    lp_allrows(X, xr[0], xr[1], xr[2], xr[3]);
+    lp_allrows(Y, yr[0], yr[1], yr[2], yr[3]);
+    // row 0: x_R Z_Q, row 1: y_R Z_Q
+    const lu prod = lp_mul(c, c.rows(xr[1], yr[1], 0u, 0u), QZ);
+    const lu diff = lp_sub(c, c.rows(QX, QY, 0u, 0u), prod);
+    return lp_row_iszero(diff, 0) && lp_row_iszero(diff, 1);
+}

@@ -45,6 +45,9 @@ static constexpr int PV_BLOCK = 256;
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
 static constexpr uint64_t PV_KEYED_MIN = 32768;   // AUTO: smaller chunks skip dedup (Straus only)
+#ifndef PV_LATENCY_MAX
+#define PV_LATENCY_MAX 2048  // AUTO: batches up to this size take the latency path (pv_latency.hip)
+#endif
 
 // ---------------------------------------------------------------------------------------- device
 
@@ -994,6 +997,7 @@ struct Ctx {
     Work work{nullptr, nullptr, nullptr, nullptr, 0};
     KeyWork kw{};
     bool last_keyed = false;  // the most recent chunk ran the dedup / split kernels
+    bool last_latency = false;  // the most recent launch took the latency path
     uint32_t last_split[3] = {0, 0, 0};  // PV_SPLIT_* of it, read back by pv_last_path
     uint4* d_bcomb = nullptr;  // fixed-base comb T_B
     int path = PV_PATH_AUTO;
@@ -1075,6 +1079,9 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
     const uint64_t cap = g_ctx.work.stride;
     const int nchunks = (int)((n + cap - 1) / cap);
     constexpr int NE = PV_NSTAGES + 1;
+    // small batches: one wave pair per request (pv_latency.hip); forced LATENCY takes it at any size
+    const bool latency = g_ctx.path == PV_PATH_LATENCY || (g_ctx.path == PV_PATH_AUTO && n <= PV_LATENCY_MAX);
+    g_ctx.last_latency = latency;
     int evb = 0;
     if (g_ctx.timing) {
         evb = g_ctx.ev_used;
@@ -1093,6 +1100,16 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         };
         int rc = mark(PV_STAGE_KEYS);
         if (rc) return rc;
+        if (latency) {
+            // one kernel: every stage of the verification inside it (timed as MSM)
+            g_ctx.last_keyed = false;
+            for (int k = PV_STAGE_PREP; k <= PV_STAGE_MSM; k++)
+                if ((rc = mark(k))) return rc;
+            rc = pv_latency_launch(d_sm, d_off + c0, m, d_pk + 32 * c0, g_ctx.d_bcomb, d_verdict + c0 / 64, stream);
+            if (rc) return rc;
+            if ((rc = mark(PV_STAGE_ENCODE)) || (rc = mark(PV_NSTAGES))) return rc;
+            continue;
+        }
         // Path split (measured round-1 costs on MI355X): a key's comb table costs ~0.47 us of device
         // time (chain + 4,128-entry fill) and then saves ~10 ns per request against the Straus
         // path (~3 vs ~13 ns), so AUTO gives a table to keys with >= PV_COMB_MIN_REQ requests in
@@ -1325,7 +1342,7 @@ int pv_last_path(int* path, uint32_t* nkeys) {
         PV_HIP(hipMemcpy(u, g_ctx.kw.nkeys, 12, hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
     }
     if (nkeys) *nkeys = u[PV_SPLIT_KEYS];
-    if (path) *path = u[PV_SPLIT_SLOTS] > 0 ? PV_PATH_COMB : PV_PATH_STRAUS;
+    if (path) *path = g_ctx.last_latency ? PV_PATH_LATENCY : u[PV_SPLIT_SLOTS] > 0 ? PV_PATH_COMB : PV_PATH_STRAUS;
     g_ctx.last_split[0] = u[PV_SPLIT_KEYS];
     g_ctx.last_split[1] = u[PV_SPLIT_COMB_KEYS];
     g_ctx.last_split[2] = u[PV_SPLIT_SLOTS];
@@ -1342,7 +1359,7 @@ int pv_last_split(uint32_t* keys, uint32_t* comb_keys, uint32_t* comb_requests) 
 }
 
 int pv_set_path(int mode) {
-    if (mode != PV_PATH_AUTO && mode != PV_PATH_STRAUS && mode != PV_PATH_COMB)
+    if (mode != PV_PATH_AUTO && mode != PV_PATH_STRAUS && mode != PV_PATH_COMB && mode != PV_PATH_LATENCY)
         return fail(PV_ERR_ARG, "pv_set_path: unknown mode");
     std::lock_guard<std::mutex> lk(g_mu);
     g_ctx.path = mode;

@@ -18,8 +18,8 @@ PV_BLOB_SLACK = 256
 PV_ABI_VERSION = 1
 
 PV_STAGES = ("keys", "prep", "table", "msm", "encode")  # PV_STAGE_* order
-PV_PATH_AUTO, PV_PATH_STRAUS, PV_PATH_COMB = 0, 1, 2
-PATH_NAMES = ("straus", "comb")  # forced arithmetic paths (tests run every one)
+PV_PATH_AUTO, PV_PATH_STRAUS, PV_PATH_COMB, PV_PATH_LATENCY = 0, 1, 2, 3
+PATH_NAMES = ("straus", "comb", "latency")  # forced arithmetic paths (tests run every one)
 
 # exported symbol -> (restype, argtypes); kept in sync with include/plenum_verify.h
 _c_u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -155,8 +155,8 @@ def verify_sm_batch(blob, offsets, pks):
 
 
 def set_path(mode):
-    """Select the arithmetic path (PV_PATH_AUTO / PV_PATH_STRAUS / PV_PATH_COMB); verdicts are
-    identical on every path."""
+    """Select the arithmetic path (PV_PATH_AUTO / PV_PATH_STRAUS / PV_PATH_COMB / PV_PATH_LATENCY);
+    verdicts are identical on every path."""
     check(lib().pv_set_path(int(mode)), "pv_set_path")
 
 

@@ -5,6 +5,7 @@
 #include "verify_core.h"
 #include "btable.h"
 #include "comb.h"
+#include "lp25519.h"
 #include <string.h>
 #include <vector>
 #include <thread>
@@ -126,7 +127,7 @@ struct HostBRows {
 
 // crypto_sign_open through the comb path: key expansion (chain + all fill blocks), radix-256
 // digits, 64 additions, batched encoding.
-int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+static const std::vector<uint32_t>& host_bcomb() {
     static std::vector<uint32_t> bcomb;
     if (bcomb.empty()) {
         bcomb.resize((size_t)PV_BCOMB_POS * PV_BCOMB_ENT * PV_BCOMB_STRIDE);
@@ -138,6 +139,11 @@ int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
                             std::cref(base[j]));
         for (auto& t : th) t.join();
     }
+    return bcomb;
+}
+
+int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    const std::vector<uint32_t>& bcomb = host_bcomb();
     std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK
     memcpy(buf.data(), sm, smlen);
     pv_sig_words in;
@@ -179,4 +185,77 @@ void hc_prepare_k(uint8_t* kout, const uint8_t* sm, uint64_t smlen, const uint8_
     pv_prepare(negA, k, in, smlen, mw);
     memcpy(kout, k, 32);
 }
+
+// ---- latency path (lp25519.h) on the host: the 64 lanes of a wave simulated exactly
+static lu hc_rows_in(const uint32_t* x /* 4 x 10 limbs */) {
+    lu v;
+    for (int l = 0; l < 64; l++) v.v[l] = (l & 15) < 10 ? x[10 * (l >> 4) + (l & 15)] : 0x1234567u + l;
+    return v;
 }
+static void hc_rows_out(uint32_t* x, const lu& v) {
+    for (int r = 0; r < 4; r++)
+        for (int k = 0; k < 10; k++) x[10 * r + k] = v.v[16 * r + k];
+}
+void hc_lp_mul(uint32_t* h, const uint32_t* f, const uint32_t* g) {
+    const LpLane c = LpLane::make();
+    hc_rows_out(h, lp_mul(c, hc_rows_in(f), hc_rows_in(g)));
+}
+void hc_lp_pow22523(uint32_t* h, const uint32_t* f) {
+    const LpLane c = LpLane::make();
+    hc_rows_out(h, lp_pow22523(c, hc_rows_in(f)));
+}
+// group ops on an ext point given as 4 rows [X, Y, Z, T]
+void hc_lp_dbl(uint32_t* out, const uint32_t* p) {
+    const LpLane c = LpLane::make();
+    hc_rows_out(out, lp_dbl(c, hc_rows_in(p)));
+}
+void hc_lp_add(uint32_t* out, const uint32_t* p, const uint32_t* q) {
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    hc_rows_out(out, lp_add_cached(c, hc_rows_in(p), lp_to_cached(c, hc_rows_in(q), K.d2)));
+}
+void hc_lp_sub(uint32_t* out, const uint32_t* p, const uint32_t* q) {
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    hc_rows_out(out, lp_add_cached(c, hc_rows_in(p), lp_neg_cached(c, lp_to_cached(c, hc_rows_in(q), K.d2))));
+}
+
+// crypto_sign_open through the latency path: the kernel's two waves, one after the other
+int hc_lp_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    const std::vector<uint32_t>& bcomb = host_bcomb();
+    std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    HostMsg mw{buf.data()};
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    // wave 1: signature side
+    uint32_t fs[8];
+    sc_recode65536(fs, in.S);
+    lu ent[PV_BCOMB_POS];
+    for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb.data(), j, pv_half(fs[j >> 1], j));
+    const bool sig_ok = pv_sig_ok(in, smlen);
+    uint32_t k[8], ek[8];
+    pv_hash_k(k, in, smlen, mw);
+    sc_recode16(ek, k);
+    const lu SB = lp_comb_b(c, [&](int j) { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); });
+    // wave 0: key side
+    lu sw[8];
+    const lm odd_row = lp_eq(c.row & 1u, 1u);
+    for (int q = 0; q < 8; q++) sw[q] = lp_sel(odd_row, in.R[q], in.A[q]);
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    const bool key_ok = pv_ge_is_canonical(in.A) && !pv_has_small_order(in.A) && dec.ok_a;
+    const bool r_ok = pv_ge_is_canonical(in.R) && dec.ok_r && !(dec.x_r_zero && (in.R[7] >> 31));
+    const lu negA = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
+    std::vector<lu> tab(17);
+    lp_build_a_table(c, K, negA, [&](int j, const lu& q) { tab[j + 8] = q; });
+    const lu QA = lp_straus_a(c, [&](int i) { return pv_nibble(ek[i >> 3], i); },
+                              [&](int e) { return tab[e + 8]; });
+    const bool eq = lp_final_check(c, K, QA, SB, dec.X, dec.Y);
+    return eq && key_ok && r_ok && sig_ok;
+}
+
+}  // extern "C"

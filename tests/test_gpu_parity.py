@@ -9,12 +9,12 @@ from vectors import VectorGen, pack
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["straus", "comb"])
+@pytest.fixture(scope="module", params=["straus", "comb", "latency"])
 def native(request):
     """The engine with each arithmetic path forced in turn (verdicts must not depend on it)."""
     from plenum_amd import _native
     _native.ensure_device()
-    _native.set_path(_native.PV_PATH_STRAUS if request.param == "straus" else _native.PV_PATH_COMB)
+    _native.set_path(getattr(_native, "PV_PATH_" + request.param.upper()))
     yield _native
     _native.set_path(_native.PV_PATH_AUTO)
 

@@ -1,0 +1,142 @@
+"""The latency path's limb-parallel arithmetic (indy-plenum_amd/csrc/lp25519.h) on the HOST: the
+64 lanes of a wave simulated exactly (DPP row broadcast / rotate / shift and the gfx950 permlane
+swaps as specified), every lp_mul column recomputed in 128 bits and bound-checked (PV_BOUNDS_CHECK),
+against Python big integers, the C oracle, the golden libsodium verdicts and libsodium itself.
+tests/test_gpu_parity.py runs the same code on the GPU (PV_PATH_LATENCY)."""
+import ctypes
+import json
+import os
+import random
+
+import pytest
+
+from test_native_host import HERE, L, P, W, from_limbs, hc, to_limbs  # noqa: F401
+
+A40 = ctypes.c_uint32 * 40
+D = (-121665 * pow(121666, P - 2, P)) % P
+
+
+def rows_in(vals):
+    out = []
+    for v in vals:
+        out += v if isinstance(v, list) else to_limbs(v)
+    return A40(*out)
+
+
+def rows_out(a):
+    a = list(a)
+    return [a[10 * r:10 * r + 10] for r in range(4)]
+
+
+def rand_limbs(rng, bound_bits):
+    return [rng.randrange(int(2 ** bound_bits)) for _ in W]
+
+
+def test_lp_mul_random_and_bounds(hc):
+    rng = random.Random(3)
+    h = A40()
+    # operand widths the group formulas produce: LR products, sums of two (2^27.13), differences
+    # with 2p (2^27.6) on either side, and the doubling's uncarried E (2^28.4) against H or F
+    combos = [(26.01, 26.01), (27.13, 27.13), (27.6, 27.6), (28.4, 27.13), (28.4, 26.01)]
+    for it in range(600):
+        fb, gb = combos[it % len(combos)]
+        f = [rand_limbs(rng, fb) for _ in range(4)]
+        g = [rand_limbs(rng, gb) for _ in range(4)]
+        if it < len(combos):
+            f = [[int(2 ** fb) - 1] * 10] * 4
+            g = [[int(2 ** gb) - 1] * 10] * 4
+        hc.hc_lp_mul(h, rows_in(f), rows_in(g))
+        for r, hr in enumerate(rows_out(h)):
+            assert from_limbs(hr) % P == from_limbs(f[r]) * from_limbs(g[r]) % P, (it, r)
+            for k, x in enumerate(hr):
+                assert x < (1 << W[k]) + (1 << 23)
+    for _ in range(200):
+        f = [rng.randrange(P) for _ in range(4)]
+        g = [rng.randrange(P) for _ in range(4)]
+        hc.hc_lp_mul(h, rows_in(f), rows_in(g))
+        for r, hr in enumerate(rows_out(h)):
+            assert from_limbs(hr) % P == f[r] * g[r] % P
+
+
+def test_lp_pow22523(hc):
+    rng = random.Random(4)
+    h = A40()
+    for _ in range(5):
+        z = [rng.randrange(P) for _ in range(4)]
+        hc.hc_lp_pow22523(h, rows_in(z))
+        for r, hr in enumerate(rows_out(h)):
+            assert from_limbs(hr) % P == pow(z[r], (P - 5) // 8, P)
+
+
+def _decode(enc):
+    """(x, y) of an Ed25519 encoding (RFC 8032 decompression)."""
+    y = int.from_bytes(enc, "little") & (2 ** 255 - 1)
+    s = enc[31] >> 7
+    u, v = (y * y - 1) % P, (D * y * y + 1) % P
+    x = u * pow(v, 3, P) * pow(u * pow(v, 7, P), (P - 5) // 8, P) % P
+    if v * x * x % P != u:
+        x = x * pow(2, (P - 1) // 4, P) % P
+    if x & 1 != s:
+        x = P - x
+    return x, y
+
+
+def _ext(pt):
+    x, y = pt
+    return [x, y, 1, x * y % P]
+
+
+def _affine(rows):
+    X, Y, Z, T = (from_limbs(r) % P for r in rows)
+    zi = pow(Z, P - 2, P)
+    assert X * Y % P == T * Z % P  # T consistent
+    return X * zi % P, Y * zi % P
+
+
+def _add(p, q):
+    (x1, y1), (x2, y2) = p, q
+    t = D * x1 * x2 * y1 * y2 % P
+    return ((x1 * y2 + x2 * y1) * pow(1 + t, P - 2, P) % P, (y1 * y2 + x1 * x2) * pow(1 - t, P - 2, P) % P)
+
+
+def test_lp_group_ops(hc, oracle):
+    rng = random.Random(5)
+    out = A40()
+    from vectors import ORDER8
+    pts = [_decode(oracle.scalarmult_base(rng.randrange(1, L).to_bytes(32, "little"))) for _ in range(6)]
+    pts += [_decode(ORDER8), (0, 1), (0, P - 1)]  # small order, identity, order 2
+    for p in pts:
+        hc.hc_lp_dbl(out, rows_in(_ext(p)))
+        assert _affine(rows_out(out)) == _add(p, p)
+        for q in pts:
+            hc.hc_lp_add(out, rows_in(_ext(p)), rows_in(_ext(q)))
+            assert _affine(rows_out(out)) == _add(p, q)
+            hc.hc_lp_sub(out, rows_in(_ext(p)), rows_in(_ext(q)))
+            assert _affine(rows_out(out)) == _add(p, ((P - q[0]) % P, q[1]))
+
+
+def _lp_open(hc, sm, pk):
+    return bool(hc.hc_lp_sign_open(sm, ctypes.c_uint64(len(sm)), pk))
+
+
+def test_lp_path_golden_verdicts(hc):
+    with open(os.path.join(HERE, "golden", "verdicts.json")) as f:
+        cases = json.load(f)
+    # every class, a bounded sample (each host-simulated verification runs ~900 lp products)
+    seen = {}
+    for c in cases:
+        seen.setdefault((c["cls"], c["ok"]), []).append(c)
+    for key, cs in sorted(seen.items()):
+        for c in cs[:3]:
+            sm, pk = bytes.fromhex(c["sm"]), bytes.fromhex(c["pk"])
+            assert _lp_open(hc, sm, pk) == c["ok"], key
+
+
+@pytest.mark.slow
+def test_lp_path_vs_libsodium(hc, sodium, oracle):
+    from vectors import VectorGen
+    g = VectorGen(sodium, oracle, seed=23)
+    for cls in VectorGen.CLASSES:
+        for _ in range(3):
+            sm, pk = g.make(cls)
+            assert _lp_open(hc, sm, pk) == sodium.sign_open_ok(sm, pk), cls
