@@ -22,8 +22,8 @@
 // The same source compiles for the host with lu/lu64/lm = 64-lane arrays and the cross-lane
 // operations simulated exactly (tests/native/hostcheck.hip, tests/test_native_host.py), with the
 // limb bounds asserted under PV_BOUNDS_CHECK. Bound names: "LR" = limb < 2^w + 2^22.6 (w = 26 even,
-// 25 odd), the output of lp_mul; lp_mul needs g limbs < 2^27.75 (19 g < 2^32), f limbs < 2^31, and
-// every column < 2^64 (checked on the host).
+// 25 odd), the output of lp_mul; lp_mul needs g's even limbs < 2^27.75 (19 g < 2^32) and odd limbs
+// < 2^27.07 (38 g < 2^32), and every column < 2^64 (checked on the host).
 #pragma once
 #include "fe25519.h"
 #include "ge25519.h"
@@ -233,22 +233,31 @@ LP_FN lu lp_carry1(const LpLane& c, const lu& x) {
     return l + in;
 }
 
-// h = f g (row by row). f limbs < 2^31, g limbs < 2^27.75; output LR.
+// h = f g (row by row). g: even limbs < 2^27.75 (19 g < 2^32), odd limbs < 2^27.07 (38 g < 2^32);
+// f: any 32-bit limbs within the column bound (every column < 2^64, checked on the host). Output LR.
+// Odd limbs are only 25 bits wide, so every g operand the group formulas form (reduced values,
+// sums of two, differences with 2p) meets the odd-limb bound, and the factor 2 of the odd x odd
+// terms is applied once to the rotated operand's odd source lanes instead of per term.
 LP_FN lu lp_mul(const LpLane& c, const lu& f, const lu& g) {
-    LP_BOUND(g, 0xD800000u, "lp_mul g operand");
-    LP_BOUND(f, 0x80000000u, "lp_mul f operand");
-    // g extended: lanes m >= 6 of Y hold 19 g_{m-6}; X = g on lanes 0..9, Y on scratch lanes 10..15
+#if !LP_DEVICE
+    for (int l = 0; l < 64; l++) {
+        if ((l & 15) >= 10) continue;
+        LP_CHECK(g.v[l] < ((l & 1) ? 0x8600000u : 0xD790000u), "lp_mul g operand");
+    }
+#endif
+    // g extended: lanes m >= 6 of Y hold 19 g_{m-6}; X = g on lanes 0..9, Y on scratch lanes 10..15;
+    // X2 / Y2: the same with odd lanes doubled (the limb index m or m - 6 has the lane's parity)
     const lu Y = lp_shr<6>(g) * 19u;
     const lu X = lp_sel(c.kge10, Y, g);
-    const lu f2 = f + f;
+    const lu X2 = lp_sel(c.keven, X, X + X);
+    const lu Y2 = lp_sel(c.keven, Y, Y + Y);
     lu64 acc = lp_mad(lp_bcast<0>(f), X, lu64(0ull));
 #define LP_TERM(I)                                                                        \
     {                                                                                     \
-        lu fi = lp_bcast<I>(f);                                                           \
-        if (I & 1) fi = lp_sel(c.keven, lp_bcast<I>(f2), fi);                             \
-        lu gi = lp_ror<I>(X);                                                             \
-        if (I >= 7) gi = lp_sel(lp_le(c.k, (uint32_t)(I - 7)), lp_ror<I>(Y), gi);         \
-        acc = lp_mad(fi, gi, acc);                                                        \
+        const lu& src = (I & 1) ? X2 : X;                                                 \
+        lu gi = lp_ror<I>(src);                                                           \
+        if (I >= 7) gi = lp_sel(lp_le(c.k, (uint32_t)(I - 7)), lp_ror<I>((I & 1) ? Y2 : Y), gi); \
+        acc = lp_mad(lp_bcast<I>(f), gi, acc);                                            \
     }
     LP_TERM(1) LP_TERM(2) LP_TERM(3) LP_TERM(4) LP_TERM(5) LP_TERM(6) LP_TERM(7) LP_TERM(8) LP_TERM(9)
 #undef LP_TERM
@@ -365,9 +374,10 @@ LP_FN lu lp_from_words(const LpLane& c, const lu s[8]) {
 
 // r = p + q (q cached or niels, possibly negated by the caller)
 LP_FN lu lp_add_cached(const LpLane& c, const lu& p, const lu& q) {
-    lu X, Y, Z, T;
-    lp_allrows(p, X, Y, Z, T);
-    const lu f = c.rows(lp_sub(c, Y, X), Y + X, T, Z);  // (Y-X, Y+X, T, Z): < 2^27.6
+    // one row exchange gives a = [X X Z Z], b = [Y Y T T]: the operand rows (Y-X, Y+X, T, Z)
+    lu a = p, b = p;
+    lp_swap16(a, b);
+    const lu f = c.rows(lp_sub(c, b, a), b + a, b, a);  // < 2^27.6
     const lu abcd = lp_mul(c, f, q);                     // [A, B, C, D]
     lu A, B, C, D;
     lp_allrows(abcd, A, B, C, D);
@@ -376,16 +386,17 @@ LP_FN lu lp_add_cached(const LpLane& c, const lu& p, const lu& q) {
     return lp_mul(c, c.rows(E, G, F, E), c.rows(F, H, G, H));
 }
 
-// r = 2 p (dbl-2008-hwcd: XX, YY, ZZ, (X+Y)^2 in the four rows at once)
+// r = 2 p (dbl-2008-hwcd with 2XY = 2TZ: rows square X, Y, Z and multiply T Z at once, so the input
+// needs no row exchange; p must carry a consistent T, which every lp operation produces)
 LP_FN lu lp_dbl(const LpLane& c, const lu& p) {
-    lu X, Y, Z, T;
-    lp_allrows(p, X, Y, Z, T);
-    const lu sq = lp_sq(c, c.rows(X, Y, Z, X + Y));  // [XX, YY, ZZ, SS]
-    lu XX, YY, ZZ, SS;
-    lp_allrows(sq, XX, YY, ZZ, SS);
-    const lu rY = YY + XX;                            // H
-    const lu rZ = lp_sub(c, YY, XX);                  // G
-    const lu rX = lp_sub4p(c, SS, rY);                // E, < 2^28.4: f side only
+    lu a = p, b = p;
+    lp_swap16(a, b);                                       // a = [X X Z Z]: row 3 gets Z
+    const lu sq = lp_mul(c, p, lp_sel(c.row3, a, p));      // [XX, YY, ZZ, TZ]
+    lu XX, YY, ZZ, TZ;
+    lp_allrows(sq, XX, YY, ZZ, TZ);
+    const lu rY = YY + XX;                                 // H
+    const lu rZ = lp_sub(c, YY, XX);                       // G
+    const lu rX = TZ + TZ;                                 // E = 2XY
     const lu rT = lp_carry1(c, lp_sub4p(c, ZZ + ZZ, rZ));  // F (carried: a g operand)
     // X3 = E F, Y3 = H G, Z3 = G F, T3 = E H
     return lp_mul(c, c.rows(rX, rY, rZ, rX), c.rows(rT, rZ, rT, rY));

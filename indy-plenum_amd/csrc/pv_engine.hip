@@ -998,6 +998,7 @@ struct Ctx {
     KeyWork kw{};
     bool last_keyed = false;  // the most recent chunk ran the dedup / split kernels
     bool last_latency = false;  // the most recent launch took the latency path
+    bool verdict_zeroed = false;  // the caller's verdict words are already 0 (pv_verify_batch)
     uint32_t last_split[3] = {0, 0, 0};  // PV_SPLIT_* of it, read back by pv_last_path
     uint4* d_bcomb = nullptr;  // fixed-base comb T_B
     int path = PV_PATH_AUTO;
@@ -1105,7 +1106,8 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             g_ctx.last_keyed = false;
             for (int k = PV_STAGE_PREP; k <= PV_STAGE_MSM; k++)
                 if ((rc = mark(k))) return rc;
-            rc = pv_latency_launch(d_sm, d_off + c0, m, d_pk + 32 * c0, g_ctx.d_bcomb, d_verdict + c0 / 64, stream);
+            rc = pv_latency_launch(d_sm, d_off + c0, m, d_pk + 32 * c0, g_ctx.d_bcomb, d_verdict + c0 / 64,
+                                   g_ctx.verdict_zeroed, stream);
             if (rc) return rc;
             if ((rc = mark(PV_STAGE_ENCODE)) || (rc = mark(PV_NSTAGES))) return rc;
             continue;
@@ -1466,15 +1468,25 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     uint8_t* d = g_ctx.d_stage;
     uint8_t* dblob = d + pk_bytes + off_bytes + v_bytes;
     hipStream_t s = g_ctx.stream;
-    PV_HIP(hipMemcpyAsync(d, h, pk_bytes + off_bytes, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-    PV_HIP(hipMemcpyAsync(dblob + blob, hblob + blob, PV_BLOB_SLACK, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-    rc = pv_stage_to_device(dblob, hblob, sm + sm_off[0], blob, s);
-    if (rc) {
-        (void)hipStreamSynchronize(s);  // no DMA may still read the staging buffer when the caller retries
-        return rc;
+    // the verdict words travel zeroed (the latency path ORs its bits into them)
+    memset(h + pk_bytes + off_bytes, 0, v_bytes);
+    if (blob < (8ull << 20)) {
+        // small batch (Plenum's quotas): one copy of the whole staging area, one DMA
+        memcpy(hblob, sm + sm_off[0], blob);
+        PV_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    } else {
+        PV_HIP(hipMemcpyAsync(d, h, pk_bytes + off_bytes + v_bytes, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpyAsync(dblob + blob, hblob + blob, PV_BLOB_SLACK, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        rc = pv_stage_to_device(dblob, hblob, sm + sm_off[0], blob, s);
+        if (rc) {
+            (void)hipStreamSynchronize(s);  // no DMA may still read the staging buffer when the caller retries
+            return rc;
+        }
     }
     uint64_t* dver = reinterpret_cast<uint64_t*>(d + pk_bytes + off_bytes);
+    g_ctx.verdict_zeroed = true;
     rc = launch(d + pk_bytes + off_bytes + v_bytes, reinterpret_cast<const uint64_t*>(d + pk_bytes), n, d, dver, s);
+    g_ctx.verdict_zeroed = false;
     if (rc) return rc;
     uint64_t* hver = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
     PV_HIP(hipMemcpyAsync(hver, dver, vwords * 8, hipMemcpyDeviceToHost, s), PV_ERR_LAUNCH);

@@ -120,11 +120,14 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 
 // Enqueue the latency path for n requests (device buffers as pv_verify_batch_device) on `stream`.
 int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
-                      const void* d_bcomb, uint64_t* d_verdict, hipStream_t stream) {
+                      const void* d_bcomb, uint64_t* d_verdict, bool verdict_zeroed, hipStream_t stream) {
     if (n == 0) return PV_OK;
     if (n > 0x7FFFFFFFull) return pv_fail(PV_ERR_ARG, "pv_latency: too many requests for one launch");
-    hipError_t e = hipMemsetAsync(d_verdict, 0, (n + 63) / 64 * 8, stream);
-    if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+    hipError_t e = hipSuccess;
+    if (!verdict_zeroed) {  // the kernel ORs its bits into the words
+        e = hipMemsetAsync(d_verdict, 0, (n + 63) / 64 * 8, stream);
+        if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+    }
     hipLaunchKernelGGL(pv_lat_kernel, dim3((unsigned)n), dim3(LAT_THREADS), 0, stream, d_sm, d_off, n, d_pk,
                        reinterpret_cast<const uint32_t*>(d_bcomb), reinterpret_cast<unsigned long long*>(d_verdict));
     e = hipGetLastError();

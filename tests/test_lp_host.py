@@ -29,7 +29,9 @@ def rows_out(a):
 
 
 def rand_limbs(rng, bound_bits):
-    return [rng.randrange(int(2 ** bound_bits)) for _ in W]
+    """Limbs below 2^bound_bits (even) / 2^(bound_bits - 1) (odd): odd limbs are 25 bits wide, so
+    every value the formulas form (sums, differences with 2p or 4p) keeps them half as large."""
+    return [rng.randrange(int(2 ** (bound_bits - (i & 1)))) for i in range(10)]
 
 
 def test_lp_mul_random_and_bounds(hc):
@@ -43,8 +45,8 @@ def test_lp_mul_random_and_bounds(hc):
         f = [rand_limbs(rng, fb) for _ in range(4)]
         g = [rand_limbs(rng, gb) for _ in range(4)]
         if it < len(combos):
-            f = [[int(2 ** fb) - 1] * 10] * 4
-            g = [[int(2 ** gb) - 1] * 10] * 4
+            f = [[int(2 ** (fb - (i & 1))) - 1 for i in range(10)]] * 4
+            g = [[int(2 ** (gb - (i & 1))) - 1 for i in range(10)]] * 4
         hc.hc_lp_mul(h, rows_in(f), rows_in(g))
         for r, hr in enumerate(rows_out(h)):
             assert from_limbs(hr) % P == from_limbs(f[r]) * from_limbs(g[r]) % P, (it, r)
