@@ -107,7 +107,7 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
  *                   one chain, [S]B from the fixed-base comb, [k](-A) by 252 doublings + 64
  *                   additions, and the comparison with R without an inversion. One kernel launch;
  *                   the fastest path for small batches (Plenum's 100 / 1,000-message quotas)
- *   PV_PATH_AUTO    (default) batches of <= 2,048 requests take the latency path; otherwise
+ *   PV_PATH_AUTO    (default) batches of <= 4,096 requests take the latency path; otherwise
  *                   per chunk of >= 32,768 requests: deduplicate keys, give a comb table
  *                   to every key with >= 48 requests in the chunk (a table costs about what ~50
  *                   requests save) and verify the other requests on the Straus path in the same

@@ -46,7 +46,7 @@ static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequenc
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
 static constexpr uint64_t PV_KEYED_MIN = 32768;   // AUTO: smaller chunks skip dedup (Straus only)
 #ifndef PV_LATENCY_MAX
-#define PV_LATENCY_MAX 2048  // AUTO: batches up to this size take the latency path (pv_latency.hip)
+#define PV_LATENCY_MAX 4096  // AUTO: batches up to this size take the latency path (pv_latency.hip)
 #endif
 
 // ---------------------------------------------------------------------------------------- device
