@@ -129,6 +129,29 @@ int pv_set_timing(int enable);
 int pv_stage_times(double* ms, int max_stages, int* launches);
 int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* launches);
 
+/* Node-side key cache (persistent across calls). A node verifies requests from a fairly stable set
+ * of signers whose verkeys it already holds (the domain ledger's NYM records,
+ * plenum/server/request_handlers/utils.py:30-39). For a cached key the latency path computes [k](-A)
+ * with 32 additions from the key's radix-256 comb table (660 KB of HBM per key, built once by the
+ * engine's key-chain and fill kernels) instead of 252 doublings + 64 additions; verdicts are
+ * unchanged (the table holds exact multiples of -A, and libsodium's key checks ran when it was built).
+ * The throughput paths (and so the benchmark's headline) never read it.
+ *   pv_key_cache_configure(capacity)  allocate room for `capacity` keys (0 = free, disabled)
+ *   pv_key_cache_put(pks, n)          host keys (n x 32 B): build and insert the missing ones, refresh
+ *                                     the present ones; least recently put keys are evicted when full.
+ *                                     Synchronous (a key table takes ~1 ms of chain latency; a batch of
+ *                                     keys is built in parallel)
+ *   pv_key_cache_clear()              drop every key (capacity kept)
+ *   pv_key_cache_enable(on)           whether launches consult the cache (default on)
+ *   pv_key_cache_stats(size, cap)     keys held / capacity
+ *   pv_key_cache_contains(pk)         1 if the 32-byte key is cached */
+int pv_key_cache_configure(uint32_t capacity);
+int pv_key_cache_put(const uint8_t* pks, uint64_t n);
+int pv_key_cache_clear(void);
+int pv_key_cache_enable(int enable);
+int pv_key_cache_stats(uint32_t* size, uint32_t* capacity);
+int pv_key_cache_contains(const uint8_t* pk);
+
 /* Batched base58 decode (Bitcoin alphabet, PyPI base58 2.x b58decode semantics: trailing ASCII
  * whitespace stripped, each leading '1' -> 0x00). Input: strings concatenated in `chars` with
  * n+1 offsets. Output: out[i * out_stride ...], out_len[i] bytes, status[i] = 0 ok, 1 invalid

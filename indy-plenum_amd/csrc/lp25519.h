@@ -546,6 +546,30 @@ LP_FN lu lp_comb_b(const LpLane& c, const Entry& entry) {
     return acc;
 }
 
+// Entry |e| of position i of a key's radix-256 comb table (comb.h: [32][129] cached points, words
+// Y+X at 0..9, Y-X at 10..19, 2Z at 20..29, 2dT at 30..39) in lp cached layout [Y-X, Y+X, 2dT, 2Z]
+// (rows 0 / 1 swapped for e < 0; lp_ctab_fix then negates 2dT). Split from the fix-up so all 32
+// loads of a verification can be issued before the first addition.
+LP_FN lu lp_ctab_load(const LpLane& c, const uint32_t* tab, int i, int e) {
+    const bool neg = e < 0;
+    const uint32_t d = (uint32_t)(neg ? -e : e);
+    const uint32_t* p = tab + ((uint32_t)i * PV_COMB_ENT + d) * 40u;
+    const lu kk = lp_sel(c.kge10, 9u, c.k);
+    return lp_gather(p, c.rows(neg ? kk : kk + 10u, neg ? kk + 10u : kk, kk + 30u, kk + 20u));
+}
+LP_FN lu lp_ctab_fix(const LpLane& c, const lu& raw, int e) {
+    return e < 0 ? lp_sel(c.row2, lp_sub(c, 0u, raw), raw) : raw;
+}
+
+// [k](-A) from a cached key table: 32 additions of T_A[i][e_i] (signed radix-256 digits e_i of k),
+// no doublings. entry(i) = the fixed-up entry of position i.
+template <class Entry>
+LP_FN lu lp_comb_a(const LpLane& c, const Entry& entry) {
+    lu acc = lp_identity_ext(c);
+    for (int i = PV_COMB_POS - 1; i >= 0; i--) acc = lp_add_cached(c, acc, entry(i));
+    return acc;
+}
+
 // The final check: Q = QA + SB (SB as ext), then libsodium's encode(Q) == R rewritten without an
 // inversion: R canonical (checked by the caller), R decompressed (X row 1 = x_R with R's sign,
 // Y row 1 = y_R), and x_R != 0 or sign 0; accept iff X_Q = x_R Z_Q and Y_Q = y_R Z_Q. Given y_Q =

@@ -13,6 +13,8 @@
 #include <stdio.h>
 #include <string.h>
 #include <algorithm>
+#include <list>
+#include <unordered_map>
 #include <mutex>
 #include <random>
 #include <atomic>
@@ -22,6 +24,7 @@
 
 #include "btable.h"
 #include "comb.h"
+#include "keycache.h"
 #include "verify_core.h"
 #include "pv_internal.h"
 #include "../../include/plenum_verify.h"
@@ -787,6 +790,26 @@ __global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kerne
     }
 }
 
+// Key cache fill: comb index j of a put batch (tables built in the workspace by the chain / fill
+// kernels) -> cache slot slots[j]: its 660 KB table, its key words and its libsodium key-check flag.
+__global__ __launch_bounds__(PV_BLOCK) void pv_kc_scatter_kernel(const uint4* __restrict__ ctab,
+                                                                  const uint32_t* __restrict__ key_flag,
+                                                                  const uint8_t* __restrict__ pk,
+                                                                  const uint32_t* __restrict__ slots, uint32_t m,
+                                                                  uint4* __restrict__ tab, uint32_t* __restrict__ flags,
+                                                                  uint32_t* __restrict__ keys) {
+    constexpr uint32_t per = PV_COMB_POS * PV_COMB_ENT * 10;  // uint4 per key table
+    const uint32_t j = blockIdx.y;
+    if (j >= m) return;
+    const uint64_t dst = (uint64_t)slots[j] * per, src = (uint64_t)j * per;
+    for (uint32_t t = blockIdx.x * PV_BLOCK + threadIdx.x; t < per; t += gridDim.x * PV_BLOCK)
+        tab[dst + t] = ctab[src + t];
+    if (blockIdx.x == 0 && threadIdx.x < 8) {
+        keys[8 * slots[j] + threadIdx.x] = reinterpret_cast<const uint32_t*>(pk)[8 * j + threadIdx.x];
+        if (threadIdx.x == 0) flags[slots[j]] = key_flag[j];
+    }
+}
+
 // Per request on the comb path: signature checks, k, key id and validity, radix-256 digits of k, S.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t* __restrict__ sm,
                                                                     const uint64_t* __restrict__ off, uint64_t n,
@@ -1014,6 +1037,22 @@ struct Ctx {
     int ev_used = 0;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // node-side key cache (keycache.h): device arrays + host index (LRU, most recent first)
+    struct {
+        uint32_t cap = 0;
+        uint32_t* d_htab = nullptr;
+        uint32_t* d_keys = nullptr;
+        uint32_t* d_flags = nullptr;
+        uint4* d_tab = nullptr;
+        uint8_t* d_put_pk = nullptr;  // keys of one put batch
+        uint32_t* d_put_slot = nullptr;
+        uint32_t hmask = 0, seed = 0;
+        bool enabled = true;  // consulted by the latency path
+        std::unordered_map<std::string, std::list<uint32_t>::iterator> index;  // key bytes -> LRU node
+        std::list<uint32_t> lru;                                                 // slots, most recent first
+        std::vector<std::string> slot_key;
+        std::vector<uint32_t> free_slots;
+    } kc;
 };
 
 Ctx g_ctx;
@@ -1030,6 +1069,43 @@ int fail(int code, const std::string& msg) {
         hipError_t e_ = (call);                                                                \
         if (e_ != hipSuccess) return fail(code, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
+
+PvKeyCacheView kc_view() {
+    PvKeyCacheView v{g_ctx.kc.d_htab, g_ctx.kc.d_keys, g_ctx.kc.d_flags, g_ctx.kc.d_tab, 0u, g_ctx.kc.seed};
+    if (g_ctx.kc.enabled && g_ctx.kc.cap > 0 && !g_ctx.kc.index.empty()) v.hmask = g_ctx.kc.hmask;
+    return v;
+}
+
+void kc_free() {
+    auto& k = g_ctx.kc;
+    for (void* p : {(void*)k.d_htab, (void*)k.d_keys, (void*)k.d_flags, (void*)k.d_tab, (void*)k.d_put_pk,
+                    (void*)k.d_put_slot})
+        if (p) (void)hipFree(p);
+    k.d_htab = k.d_keys = k.d_flags = k.d_put_slot = nullptr;
+    k.d_tab = nullptr;
+    k.d_put_pk = nullptr;
+    k.cap = k.hmask = 0;
+    k.index.clear();
+    k.lru.clear();
+    k.slot_key.clear();
+    k.free_slots.clear();
+}
+
+// Rebuild the open-addressing table from the index and upload it (stream-ordered).
+int kc_upload_htab(hipStream_t s) {
+    auto& k = g_ctx.kc;
+    std::vector<uint32_t> h((size_t)k.hmask + 1, PV_KC_EMPTY);
+    for (auto& e : k.index) {
+        uint32_t A[8];
+        memcpy(A, e.first.data(), 32);
+        uint32_t p = pv_kc_hash(A, k.seed) & k.hmask;
+        while (h[p] != PV_KC_EMPTY) p = (p + 1) & k.hmask;
+        h[p] = *e.second;
+    }
+    PV_HIP(hipMemcpyAsync(k.d_htab, h.data(), h.size() * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // h is a local buffer
+    return PV_OK;
+}
 
 int ensure_stage(uint64_t host_bytes, uint64_t dev_bytes) {
     if (host_bytes > g_ctx.h_stage_cap) {
@@ -1106,8 +1182,8 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             g_ctx.last_keyed = false;
             for (int k = PV_STAGE_PREP; k <= PV_STAGE_MSM; k++)
                 if ((rc = mark(k))) return rc;
-            rc = pv_latency_launch(d_sm, d_off + c0, m, d_pk + 32 * c0, g_ctx.d_bcomb, d_verdict + c0 / 64,
-                                   g_ctx.verdict_zeroed, stream);
+            rc = pv_latency_launch(d_sm, d_off + c0, m, d_pk + 32 * c0, g_ctx.d_bcomb, kc_view(),
+                                   d_verdict + c0 / 64, g_ctx.verdict_zeroed, stream);
             if (rc) return rc;
             if ((rc = mark(PV_STAGE_ENCODE)) || (rc = mark(PV_NSTAGES))) return rc;
             continue;
@@ -1308,6 +1384,7 @@ void pv_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_ctx.device < 0) return;
     if (g_ctx.comm) ncclCommDestroy(g_ctx.comm);
+    kc_free();
     if (g_ctx.h_stage) (void)hipHostFree(g_ctx.h_stage);
     if (g_ctx.d_stage) (void)hipFree(g_ctx.d_stage);
     if (g_ctx.d_btab) (void)hipFree(g_ctx.d_btab);
@@ -1548,6 +1625,144 @@ int pv_sync(void) {
     PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
     return PV_OK;
 }
+int pv_key_cache_configure(uint32_t capacity) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_configure: call pv_init first");
+    PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);  // no launch may still read the old tables
+    kc_free();
+    if (capacity == 0) return PV_OK;
+    if (capacity > (1u << 20)) return fail(PV_ERR_ARG, "pv_key_cache_configure: capacity above 2^20 keys");
+    auto& k = g_ctx.kc;
+    uint32_t H = 2;
+    while (H < 2 * capacity) H <<= 1;
+    const uint64_t per = (uint64_t)PV_COMB_POS * PV_COMB_ENT * 160;  // bytes per key table
+    hipError_t e;
+    if ((e = hipMalloc((void**)&k.d_tab, per * capacity)) != hipSuccess ||
+        (e = hipMalloc((void**)&k.d_keys, (uint64_t)capacity * 32)) != hipSuccess ||
+        (e = hipMalloc((void**)&k.d_flags, (uint64_t)capacity * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&k.d_htab, (uint64_t)H * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&k.d_put_pk, (uint64_t)g_ctx.kw.kcap * 32)) != hipSuccess ||
+        (e = hipMalloc((void**)&k.d_put_slot, (uint64_t)g_ctx.kw.kcap * 4)) != hipSuccess) {
+        kc_free();
+        return fail(PV_ERR_ALLOC, std::string("pv_key_cache_configure: hipMalloc: ") + hipGetErrorString(e));
+    }
+    k.cap = capacity;
+    k.hmask = H - 1;
+    k.seed = (uint32_t)std::random_device{}() | 1u;
+    k.slot_key.assign(capacity, std::string());
+    for (uint32_t i = capacity; i-- > 0;) k.free_slots.push_back(i);
+    return kc_upload_htab(g_ctx.stream);
+}
+
+int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& k = g_ctx.kc;
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: call pv_init first");
+    if (k.cap == 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: cache not configured");
+    if (n > 0 && !pks) return fail(PV_ERR_ARG, "pv_key_cache_put: null pointer");
+    // slots for the new keys (at most cap of them: the last cap distinct keys of the call win)
+    std::vector<std::string> fresh;
+    std::vector<uint32_t> fresh_slot;
+    for (uint64_t i = 0; i < n; i++) {
+        std::string key(reinterpret_cast<const char*>(pks + 32 * i), 32);
+        auto it = k.index.find(key);
+        if (it != k.index.end()) {  // refresh
+            k.lru.splice(k.lru.begin(), k.lru, it->second);
+            continue;
+        }
+        uint32_t slot;
+        if (!k.free_slots.empty()) {
+            slot = k.free_slots.back();
+            k.free_slots.pop_back();
+        } else {  // evict the least recently put key
+            slot = k.lru.back();
+            k.lru.pop_back();
+            k.index.erase(k.slot_key[slot]);
+            for (size_t f = 0; f < fresh.size(); f++)
+                if (fresh_slot[f] == slot) fresh_slot[f] = PV_KC_EMPTY;  // evicted before it was built
+        }
+        k.lru.push_front(slot);
+        k.index[key] = k.lru.begin();
+        k.slot_key[slot] = key;
+        fresh.push_back(key);
+        fresh_slot.push_back(slot);
+    }
+    // build the new keys' tables in batches of the workspace's comb capacity
+    hipStream_t s = g_ctx.stream;
+    if (g_ctx.last_stream && g_ctx.last_stream != s) PV_HIP(hipStreamWaitEvent(s, g_ctx.ev_launch_done, 0), PV_ERR_LAUNCH);
+    KeyWork kw = g_ctx.kw;
+    std::vector<uint32_t> ident(kw.kcap);
+    for (uint32_t j = 0; j < kw.kcap; j++) ident[j] = j;
+    PV_HIP(hipMemcpyAsync(kw.comb_key, ident.data(), (uint64_t)kw.kcap * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    PV_HIP(hipMemcpyAsync(kw.key_owner, ident.data(), (uint64_t)kw.kcap * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    std::vector<uint8_t> bpk;
+    std::vector<uint32_t> bslot;
+    for (size_t f0 = 0; f0 < fresh.size();) {
+        bpk.clear();
+        bslot.clear();
+        size_t f = f0;
+        for (; f < fresh.size() && bslot.size() < kw.kcap; f++) {
+            if (fresh_slot[f] == PV_KC_EMPTY) continue;
+            bpk.insert(bpk.end(), fresh[f].begin(), fresh[f].end());
+            bslot.push_back(fresh_slot[f]);
+        }
+        f0 = f;
+        const uint32_t m = (uint32_t)bslot.size();
+        if (m == 0) continue;
+        const uint32_t cnt[3] = {m, m, 0};
+        PV_HIP(hipMemcpyAsync(k.d_put_pk, bpk.data(), bpk.size(), hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpyAsync(k.d_put_slot, bslot.data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, 12, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        const Gate gate{kw.nkeys, kw.slot_req};
+        hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * m + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0, s,
+                           k.d_put_pk, kw, gate);
+        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        const uint64_t items = (uint64_t)m * PV_COMB_POS * PV_COMB_BLOCKS;
+        hipLaunchKernelGGL(pv_key_fill_kernel, dim3((unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096)),
+                           dim3(PV_BLOCK), 0, s, kw, gate);
+        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        hipLaunchKernelGGL(pv_kc_scatter_kernel, dim3(64, m), dim3(PV_BLOCK), 0, s, kw.ctab, kw.key_flag, k.d_put_pk,
+                           k.d_put_slot, m, k.d_tab, k.d_flags, k.d_keys);
+        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // bpk / bslot / cnt are host locals
+    }
+    g_ctx.last_keyed = false;
+    PV_HIP(hipEventRecord(g_ctx.ev_launch_done, s), PV_ERR_LAUNCH);
+    g_ctx.last_stream = s;
+    return kc_upload_htab(s);
+}
+
+int pv_key_cache_clear(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& k = g_ctx.kc;
+    if (k.cap == 0) return PV_OK;
+    PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
+    k.index.clear();
+    k.lru.clear();
+    k.free_slots.clear();
+    for (uint32_t i = k.cap; i-- > 0;) k.free_slots.push_back(i);
+    return kc_upload_htab(g_ctx.stream);
+}
+
+int pv_key_cache_enable(int enable) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_ctx.kc.enabled = enable != 0;
+    return PV_OK;
+}
+
+int pv_key_cache_stats(uint32_t* size, uint32_t* capacity) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (size) *size = (uint32_t)g_ctx.kc.index.size();
+    if (capacity) *capacity = g_ctx.kc.cap;
+    return PV_OK;
+}
+
+int pv_key_cache_contains(const uint8_t* pk) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!pk) return 0;
+    return g_ctx.kc.index.count(std::string(reinterpret_cast<const char*>(pk), 32)) ? 1 : 0;
+}
+
 int pv_stream_create(void** stream) {
     if (!stream) return fail(PV_ERR_ARG, "pv_stream_create: null pointer");
     hipStream_t s = nullptr;

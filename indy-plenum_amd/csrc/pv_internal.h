@@ -13,7 +13,9 @@ int pv_fail(int code, const std::string& msg);
 // A caller stream is being destroyed: the ingress workspace stops handing over through it.
 void pv_ingress_forget_stream(void* stream);
 // The latency path (pv_latency.hip): n requests on device buffers, verdict words written on `stream`.
+struct PvKeyCacheView;
 int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
-                      const void* d_bcomb, uint64_t* d_verdict, bool verdict_zeroed, hipStream_t stream);
+                      const void* d_bcomb, const PvKeyCacheView& kc, uint64_t* d_verdict, bool verdict_zeroed,
+                      hipStream_t stream);
 
 #endif  // PV_INTERNAL_H

@@ -9,9 +9,13 @@
 //           engine's fixed-base comb T_B (16 table additions, the 16 entries fetched up front)
 //   wave 0  key side, at the same time: decompression of A (row 0, negated) and of R (row 1) in one
 //           x^((p-5)/8) chain, the key checks, and the table [j](-A), j = -8..8, into LDS
-//   --- barrier ---
-//   wave 0  [k](-A) (63 x 4 doublings + 64 additions), Q = [S]B + [k](-A), and the comparison with R
-//           without an inversion (lp_final_check), then the request's verdict bit (atomic OR).
+//   --- barrier 1 (k ready) ---
+//   wave 0  [k](-A): 63 x 4 doublings + 64 additions, or, when the key is in the node-side key cache
+//           (keycache.h), 32 additions from its comb table and no doublings
+//   wave 1  [S]B meanwhile
+//   --- barrier 2 ([S]B ready) ---
+//   wave 0  Q = [S]B + [k](-A) and the comparison with R without an inversion (lp_final_check), then
+//           the request's verdict bit (atomic OR).
 //
 // The throughput paths keep one verification per lane and need ~1 ms however small the batch; here
 // the serial chain of one verification is spread over a wave (lp25519.h), so a batch of up to a few
@@ -20,6 +24,7 @@
 #include <stdint.h>
 
 #include "comb.h"
+#include "keycache.h"
 #include "lp25519.h"
 #include "verify_core.h"
 #include "pv_internal.h"
@@ -42,13 +47,14 @@ struct LatMsg {
 __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __restrict__ sm,
                                                               const uint64_t* __restrict__ off, uint64_t n,
                                                               const uint8_t* __restrict__ pk,
-                                                              const uint32_t* __restrict__ bcomb,
+                                                              const uint32_t* __restrict__ bcomb, PvKeyCacheView kc,
                                                               unsigned long long* __restrict__ verdict) {
 #if LP_DEVICE  // the lp types are 64-lane host arrays in the host pass: the body is device-only
     const uint32_t r = blockIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    __shared__ uint32_t s_k[8];            // signed radix-16 digits of k
+    __shared__ uint32_t s_k16[8];          // signed radix-16 digits of k (Straus, key not cached)
+    __shared__ uint32_t s_k256[8];         // signed radix-256 digits of k (cached key's comb table)
     __shared__ uint32_t s_sig_ok;          // libsodium's checks on R, S, smlen
     __shared__ uint32_t s_sb[64];          // [S]B, ext layout, one word per lane
     __shared__ uint32_t s_tab[17][64];     // [j](-A), j = -8..8, cached layout
@@ -72,44 +78,65 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
     const LpLane c = LpLane::make();
     const LpConsts K = LpConsts::make(c);
 
-    LpDecomp dec;
-    bool key_ok = false, r_ok = false;
     if (wave == 1) {
-        // the 16 fixed-base entries, lp cached layout [y-x, y+x, 2dxy, 2] (negated for f < 0)
+        // signature side: the 16 fixed-base entries are fetched first, then k, then [S]B
         uint32_t fs[8];
         sc_recode65536(fs, in.S);
         lu ent[PV_BCOMB_POS];
 #pragma unroll
         for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
-        bool sig_ok = pv_sig_ok(in, smlen);
+        const bool sig_ok = pv_sig_ok(in, smlen);
         uint32_t k[8];
         pv_hash_k(k, in, smlen, mw);
-        uint32_t ek[8];
-        sc_recode16(ek, k);
+        uint32_t e16[8], e256[8];
+        sc_recode16(e16, k);
+        sc_recode256(e256, k);
         if (lane == 0) {
 #pragma unroll
-            for (int q = 0; q < 8; q++) s_k[q] = ek[q];
+            for (int q = 0; q < 8; q++) {
+                s_k16[q] = e16[q];
+                s_k256[q] = e256[q];
+            }
             s_sig_ok = sig_ok ? 1u : 0u;
         }
+        __syncthreads();  // 1: k is ready
         auto entry = [&](int j) -> lu { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); };
         s_sb[lane] = lp_comb_b(c, entry);
-    } else {
-        // rows 0 / 2: A's encoding, rows 1 / 3: R's
-        lu sw[8];
-        const lm odd_row = lp_eq(c.row & 1u, 1u);
+        __syncthreads();  // 2: [S]B is ready
+        return;
+    }
+    // key side: decompression of A (row 0) and R (row 1) in one chain
+    lu sw[8];
+    const lm odd_row = lp_eq(c.row & 1u, 1u);
 #pragma unroll
-        for (int q = 0; q < 8; q++) sw[q] = lp_sel(odd_row, in.R[q], in.A[q]);
-        dec = lp_decompress_ar(c, K, sw);
+    for (int q = 0; q < 8; q++) sw[q] = lp_sel(odd_row, in.R[q], in.A[q]);
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    const bool r_ok = pv_ge_is_canonical(in.R) && dec.ok_r && !(dec.x_r_zero && (in.R[7] >> 31));
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(pv_kc_lookup(kc, in.A));  // uniform: one branch per wave
+    bool key_ok;
+    lu QA;
+    if (slot != PV_KC_EMPTY) {
+        // cached key: libsodium's key checks ran when its table was built; [k](-A) = 32 additions
+        key_ok = kc.flags[slot] != 0;
+        const uint32_t* tab = reinterpret_cast<const uint32_t*>(kc.tab + (uint64_t)slot * PV_COMB_POS * PV_COMB_ENT * 10);
+        __syncthreads();  // 1
+        uint32_t e256[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) e256[q] = s_k256[q];
+        lu ent[PV_COMB_POS];
+#pragma unroll
+        for (int i = 0; i < PV_COMB_POS; i++) ent[i] = lp_ctab_load(c, tab, i, pv_byte(e256[i >> 2], i));
+        QA = lp_comb_a(c, [&](int i) { return lp_ctab_fix(c, ent[i], pv_byte(e256[i >> 2], i)); });
+    } else {
         key_ok = pv_ge_is_canonical(in.A) && !pv_has_small_order(in.A) && dec.ok_a;
-        r_ok = pv_ge_is_canonical(in.R) && dec.ok_r && !(dec.x_r_zero && (in.R[7] >> 31));
         const lu negA = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
         lp_build_a_table(c, K, negA, [&](int j, const lu& q) { s_tab[j + 8][lane] = q; });
+        __syncthreads();  // 1
+        auto digit = [&](int i) { return pv_nibble(s_k16[i >> 3], i); };
+        auto load = [&](int e) -> lu { return s_tab[e + 8][lane]; };
+        QA = lp_straus_a(c, digit, load);
     }
-    __syncthreads();
-    if (wave != 0) return;
-    auto digit = [&](int i) { return pv_nibble(s_k[i >> 3], i); };
-    auto load = [&](int e) -> lu { return s_tab[e + 8][lane]; };
-    const lu QA = lp_straus_a(c, digit, load);
+    __syncthreads();  // 2
     const bool eq = lp_final_check(c, K, QA, s_sb[lane], dec.X, dec.Y);
     const bool ok = eq && key_ok && r_ok && s_sig_ok != 0;
     if (lane == 0 && ok) atomicOr(&verdict[r >> 6], 1ull << (r & 63));
@@ -120,7 +147,8 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 
 // Enqueue the latency path for n requests (device buffers as pv_verify_batch_device) on `stream`.
 int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
-                      const void* d_bcomb, uint64_t* d_verdict, bool verdict_zeroed, hipStream_t stream) {
+                      const void* d_bcomb, const PvKeyCacheView& kc, uint64_t* d_verdict, bool verdict_zeroed,
+                      hipStream_t stream) {
     if (n == 0) return PV_OK;
     if (n > 0x7FFFFFFFull) return pv_fail(PV_ERR_ARG, "pv_latency: too many requests for one launch");
     hipError_t e = hipSuccess;
@@ -129,7 +157,7 @@ int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, co
         if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
     }
     hipLaunchKernelGGL(pv_lat_kernel, dim3((unsigned)n), dim3(LAT_THREADS), 0, stream, d_sm, d_off, n, d_pk,
-                       reinterpret_cast<const uint32_t*>(d_bcomb), reinterpret_cast<unsigned long long*>(d_verdict));
+                       reinterpret_cast<const uint32_t*>(d_bcomb), kc, reinterpret_cast<unsigned long long*>(d_verdict));
     e = hipGetLastError();
     if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("pv_lat_kernel: ") + hipGetErrorString(e));
     return PV_OK;

@@ -66,6 +66,12 @@ SIGNATURES = {
     "pv_memcpy_h2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "pv_memcpy_d2h": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "pv_sync": (ctypes.c_int, []),
+    "pv_key_cache_configure": (ctypes.c_int, [ctypes.c_uint32]),
+    "pv_key_cache_put": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "pv_key_cache_clear": (ctypes.c_int, []),
+    "pv_key_cache_enable": (ctypes.c_int, [ctypes.c_int]),
+    "pv_key_cache_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
+    "pv_key_cache_contains": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_stream_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "pv_stream_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_stream_sync": (ctypes.c_int, [ctypes.c_void_p]),
@@ -219,3 +225,44 @@ def ingress_verify(sigs, msgs, msg_idx, signer_idx, idrs, vks):
     vkp = np.array([v is not None for v in vks], dtype=np.uint8)
     return ingress_verify_arrays(sig_b, sig_o, msg_b, msg_o, np.asarray(msg_idx, np.uint32),
                                  np.asarray(signer_idx, np.uint32), idr_b, idr_o, vk_b, vk_o, vkp)
+
+
+class KeyCache:
+    """The engine's node-side key cache (include/plenum_verify.h pv_key_cache_*): known signers'
+    keys verified with 32 comb-table additions on the latency path instead of 252 doublings."""
+
+    @staticmethod
+    def configure(capacity):
+        ensure_device()
+        check(lib().pv_key_cache_configure(int(capacity)), "pv_key_cache_configure")
+
+    @staticmethod
+    def put(pks):
+        """pks: iterable of 32-byte keys, or a uint8 array (n, 32)."""
+        ensure_device()
+        a = np.frombuffer(b"".join(pks), np.uint8) if not isinstance(pks, np.ndarray) else pks
+        a = np.ascontiguousarray(a, np.uint8).reshape(-1)
+        if a.size % 32:
+            raise ValueError("keys must be 32 bytes each")
+        n = a.size // 32
+        check(lib().pv_key_cache_put(_ptr(a if a.size else np.zeros(32, np.uint8)), n), "pv_key_cache_put")
+
+    @staticmethod
+    def clear():
+        check(lib().pv_key_cache_clear(), "pv_key_cache_clear")
+
+    @staticmethod
+    def enable(on=True):
+        check(lib().pv_key_cache_enable(1 if on else 0), "pv_key_cache_enable")
+
+    @staticmethod
+    def stats():
+        size, cap = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().pv_key_cache_stats(ctypes.byref(size), ctypes.byref(cap)), "pv_key_cache_stats")
+        return size.value, cap.value
+
+    @staticmethod
+    def contains(pk):
+        b = np.frombuffer(bytes(pk), np.uint8)
+        return bool(lib().pv_key_cache_contains(_ptr(b)))
+

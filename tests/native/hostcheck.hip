@@ -258,4 +258,48 @@ int hc_lp_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     return eq && key_ok && r_ok && sig_ok;
 }
 
+// the cache-hit branch: [k](-A) as 32 additions from the key's comb table (built on the host with
+// the same chain / fill code the engine's key kernels run)
+int hc_lp_sign_open_cached(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    const std::vector<uint32_t>& bcomb = host_bcomb();
+    std::vector<uint8_t> buf(smlen + 256, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    HostMsg mw{buf.data()};
+    // the cache build: key checks + table (pv_key_chain_quad_kernel / pv_key_fill_kernel)
+    ge_p3 negA;
+    const bool key_ok = pv_key_ok_negate(negA, in.A);
+    std::vector<ge_p3> bases(PV_COMB_POS * PV_COMB_PTS);
+    pv_comb_chain(HostBases{bases.data()}, negA);
+    std::vector<uint32_t> ctab((size_t)PV_COMB_POS * PV_COMB_ENT * 40);
+    for (int pos = 0; pos < PV_COMB_POS; pos++)
+        for (int b = 0; b < PV_COMB_BLOCKS; b++)
+            pv_comb_fill_block(HostCombRow{ctab.data() + (size_t)pos * PV_COMB_ENT * 40},
+                               HostBasePts{bases.data() + pos * PV_COMB_PTS}, b);
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    uint32_t fs[8];
+    sc_recode65536(fs, in.S);
+    lu ent[PV_BCOMB_POS];
+    for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb.data(), j, pv_half(fs[j >> 1], j));
+    const bool sig_ok = pv_sig_ok(in, smlen);
+    uint32_t k[8], e256[8];
+    pv_hash_k(k, in, smlen, mw);
+    sc_recode256(e256, k);
+    const lu SB = lp_comb_b(c, [&](int j) { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); });
+    lu sw[8];
+    const lm odd_row = lp_eq(c.row & 1u, 1u);
+    for (int q = 0; q < 8; q++) sw[q] = lp_sel(odd_row, in.R[q], in.A[q]);
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    const bool r_ok = pv_ge_is_canonical(in.R) && dec.ok_r && !(dec.x_r_zero && (in.R[7] >> 31));
+    lu ta[PV_COMB_POS];
+    for (int i = 0; i < PV_COMB_POS; i++) ta[i] = lp_ctab_load(c, ctab.data(), i, pv_byte(e256[i >> 2], i));
+    const lu QA = lp_comb_a(c, [&](int i) { return lp_ctab_fix(c, ta[i], pv_byte(e256[i >> 2], i)); });
+    const bool eq = lp_final_check(c, K, QA, SB, dec.X, dec.Y);
+    return eq && key_ok && r_ok && sig_ok;
+}
+
 }  // extern "C"

@@ -142,3 +142,16 @@ def test_lp_path_vs_libsodium(hc, sodium, oracle):
         for _ in range(3):
             sm, pk = g.make(cls)
             assert _lp_open(hc, sm, pk) == sodium.sign_open_ok(sm, pk), cls
+
+
+def test_lp_cached_key_path_golden_verdicts(hc):
+    """The key-cache branch of the latency kernel (32 comb-table additions for [k](-A))."""
+    with open(os.path.join(HERE, "golden", "verdicts.json")) as f:
+        cases = json.load(f)
+    seen = {}
+    for c in cases:
+        seen.setdefault((c["cls"], c["ok"]), []).append(c)
+    for key, cs in sorted(seen.items()):
+        for c in cs[:2]:
+            sm, pk = bytes.fromhex(c["sm"]), bytes.fromhex(c["pk"])
+            assert bool(hc.hc_lp_sign_open_cached(sm, ctypes.c_uint64(len(sm)), pk)) == c["ok"], key

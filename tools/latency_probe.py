@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--sizes", default="1,10,100,1000,2048,4096")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--paths", default="latency,straus,auto")
+    ap.add_argument("--warm", action="store_true",
+                    help="also measure the latency path with the 1,024 signer keys in the node-side key cache")
     args = ap.parse_args()
     sizes = [int(x) for x in args.sizes.split(",")]
     nmax = max(sizes)
@@ -41,7 +43,13 @@ def main():
     _native.ensure_device()
     L = _native.lib()
     out = {"requests_signers": 1024, "tampered_every": 16, "results": {}}
-    for pname in args.paths.split(","):
+    runs = [(p, False) for p in args.paths.split(",")] + ([("latency", True)] if args.warm else [])
+    for pname, warm in runs:
+        if warm:
+            t0 = time.perf_counter()
+            _native.KeyCache.configure(2048)
+            _native.KeyCache.put([p["vk"] for p in nym_workload._pool()])
+            out["key_cache_put_1024_keys_s"] = round(time.perf_counter() - t0, 3)
         mode = getattr(_native, "PV_PATH_" + pname.upper())
         _native.set_path(mode)
         res = {}
@@ -66,8 +74,10 @@ def main():
             res[str(n)] = {"median_ms": round(1e3 * float(np.median(ts)), 4), "min_ms": round(1e3 * min(ts), 4),
                            "device_ms": round(dev_ms, 4), "path_taken": path, "ok": ok,
                            "verifies_per_s": round(n / float(np.median(ts)), 1)}
-            print(pname, n, res[str(n)], file=sys.stderr, flush=True)
-        out["results"][pname] = res
+            print(pname + ("_warm" if warm else ""), n, res[str(n)], file=sys.stderr, flush=True)
+        out["results"][pname + ("_warm_key_cache" if warm else "")] = res
+        if warm:
+            _native.KeyCache.configure(0)
     _native.set_path(_native.PV_PATH_AUTO)
     print(json.dumps(out), flush=True)
 
