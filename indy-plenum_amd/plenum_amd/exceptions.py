@@ -125,3 +125,29 @@ class NoAuthenticatorFound(SigningException):
 class InvalidKey(Exception):
     code = 142
     reason = 'invalid key'
+
+
+# plenum/common/exceptions.py:184-235: the message-validation exceptions the feed points raise
+class InvalidMessageException(BaseExc):
+    pass
+
+
+class InvalidNodeMessageException(InvalidMessageException):
+    pass
+
+
+class InvalidClientMessageException(InvalidMessageException):
+    def __init__(self, identifier, reqId, reason=None, code=None):
+        self.code = code
+        self.identifier = identifier
+        self.reqId = reqId
+        self.reason = reason
+
+
+class InvalidNodeMsg(InvalidNodeMessageException):
+    pass
+
+
+class InvalidClientRequest(InvalidClientMessageException):
+    pass
+

@@ -12,6 +12,10 @@ and stubs for zmq/jsonpickle that the hot path never calls. Outputs (all JSON, d
   verdicts.json      libsodium crypto_sign_open verdicts on normal + adversarial (sm, pk) vectors
   request.json       Request(**json.loads(text)): signing bytes of as_dict minus the excluded keys,
                      digest, payload_digest (the wire path's C++ serializer and Request mirror)
+  feed.json          the node's feed points (plenum_amd/feed.py): a client quota through
+                     Node.handleOneClientMsg and PROPAGATEs through Node.handleOneNodeMsg — the
+                     reference's own methods, compiled from plenum/server/node.py's source and run
+                     on a stub node (node.py itself cannot be imported here: ursa, rocksdb absent)
 Run all generators, or name some: python tests/golden/make_golden.py request.json
 """
 import json
@@ -341,9 +345,204 @@ def gen_request():
     return out
 
 
+# ----------------------------------------------------------------------------- feed points
+def _node_methods():
+    """Node's feed-point methods, compiled from the reference's source text and bound to a stub:
+    handleOneClientMsg, validateClientMsg, handleInvalidClientMsg, _specific_invalid_client_msg_handling,
+    handleOneNodeMsg, validateNodeMsg, verifySignature, authNr (plenum/server/node.py)."""
+    import ast
+    import contextlib
+    from collections.abc import Mapping
+    from plenum.common import exceptions as E
+    from plenum.common.constants import LEDGER_STATUS, OP_FIELD_NAME
+    from plenum.common.messages.internal_messages import PreSigVerification
+    from plenum.common.messages.node_message_factory import node_message_factory
+    from plenum.common.messages.node_messages import Batch, CatchupReq, LedgerStatus, Propagate
+    from plenum.common.txn_util import TxnUtilConfig, idr_from_req_data
+    from plenum.common.types import OPERATION, f
+    from plenum.common.util import friendlyEx, reasonForClientFromException
+    with open(os.path.join(REF, "plenum", "server", "node.py")) as fh:
+        tree = ast.parse(fh.read())
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Node")
+    want = {"handleOneClientMsg", "validateClientMsg", "handleInvalidClientMsg",
+            "_specific_invalid_client_msg_handling", "handleOneNodeMsg", "validateNodeMsg", "verifySignature",
+            "authNr"}
+    funcs = [fn for fn in cls.body if isinstance(fn, ast.FunctionDef) and fn.name in want]
+    assert {fn.name for fn in funcs} == want
+    for fn in funcs:
+        fn.decorator_list = []  # metrics decorators
+
+    class _Log:
+        def __getattr__(self, name):
+            return lambda *a, **k: None
+
+    class _Metrics:
+        def measure_time(self, *a):
+            return contextlib.nullcontext()
+
+    class _MN:
+        def __getattr__(self, name):
+            return name
+
+    ns = dict(f=f, OPERATION=OPERATION, OP_FIELD_NAME=OP_FIELD_NAME, LEDGER_STATUS=LEDGER_STATUS, Batch=Batch,
+              LedgerStatus=LedgerStatus, CatchupReq=CatchupReq, Propagate=Propagate,
+              node_message_factory=node_message_factory, PreSigVerification=PreSigVerification,
+              TxnUtilConfig=TxnUtilConfig, idr_from_req_data=idr_from_req_data, friendlyEx=friendlyEx,
+              reasonForClientFromException=reasonForClientFromException, Request=Request, Mapping=Mapping,
+              MetricsName=_MN(), logger=_Log(), **{n: getattr(E, n) for n in dir(E) if not n.startswith("_")})
+    exec(compile(ast.Module(body=funcs, type_ignores=[]), "reference:plenum/server/node.py", "exec"), ns)
+    return {fn.name: ns[fn.name] for fn in funcs}, _Metrics, Batch
+
+
+class _StubNode:
+    """What the feed-point methods touch on a Node; records the side effects."""
+
+    def __init__(self, methods, metrics_cls, whitelist, req_authnr):
+        import types
+        for name, fn in methods.items():
+            setattr(self, name, types.MethodType(fn, self))
+        self.metrics = metrics_cls()
+        self.authnWhitelist = whitelist
+        self.clientAuthNr = req_authnr
+        self.client_request_class = Request
+        self.events = []
+
+        class _Replicas:
+            def send_to_internal_bus(self, *a):
+                pass
+
+        class _Replica:
+            instId = 0
+
+        class _Stack:
+            name = "NodeC"
+        self.replicas, self.master_replica, self.clientstack = _Replicas(), _Replica(), _Stack()
+
+    def isClientBlacklisted(self, frm):
+        return False
+
+    def isNodeBlacklisted(self, frm):
+        return False
+
+    def doStaticValidation(self, msg):
+        pass
+
+    def unpackClientMsg(self, msg, frm):
+        self.events.append({"ev": "accepted", "frm": frm})
+
+    def send_nack_to_client(self, idr_reqid, reason, frm):
+        self.events.append({"ev": "nack", "frm": frm, "identifier": idr_reqid[0], "reqId": idr_reqid[1],
+                            "reason": reason})
+
+    def discard(self, msg, reason, logMethod=None, cliOutput=False):
+        self.events.append({"ev": "discard", "reason": str(reason), "exc": type(reason).__name__})
+
+    def reportSuspiciousClient(self, frm, friendly):
+        self.events.append({"ev": "suspicious_client", "frm": frm})
+
+    def reportSuspiciousNodeEx(self, ex):
+        self.events.append({"ev": "suspicious_node", "node": ex.node, "code": ex.code, "reason": ex.reason,
+                            "cause": type(ex.__cause__).__name__, "cause_str": str(ex.__cause__)})
+
+    def unpackNodeMsg(self, msg, frm):
+        self.events.append({"ev": "accepted", "frm": frm})
+
+    def _invalid_client_ledger_status_handling(self, ex, msg, frm):
+        pass
+
+
+def gen_feed():
+    methods, metrics_cls, Batch = _node_methods()
+    signers = [DidSigner(seed=("feedsigner%022d" % i).encode()) for i in range(4)]
+    clients = {s.identifier: s.verkey for s in signers[:3]}
+    bad_vk = DidSigner(seed=b"v" * 32)
+    clients[bad_vk.identifier] = "~" + "1" * 5  # abbreviated verkey too short -> InvalidKey
+    unknown = DidSigner(seed=b"n" * 32)
+
+    def fresh_authnr():
+        core = CoreAuthNr(["1", "101"], ["105"], ["action"], state=RefState({}))
+        for idr, vk in clients.items():
+            core.addIdr(idr, vk)
+        ra = ReqAuthenticator()
+        ra.register_authenticator(core)
+        spy = {"calls": 0, "ids": []}
+        orig = ra.authenticate
+
+        def authenticate(req_data, key=None):
+            spy["calls"] += 1
+            r = orig(req_data, key)
+            spy["ids"].append(sorted(r))
+            return r
+        ra.authenticate = authenticate
+        return ra, core, spy
+
+    reqs = []
+    for i, s in enumerate(signers[:3]):
+        reqs.append(("valid", signed_request(s, 100 + i)))
+    reqs.append(("duplicate", json.loads(json.dumps(reqs[0][1]))))  # verified-request cache hit
+    r = signed_request(signers[0], 110)
+    r["reqId"] += 1
+    reqs.append(("tampered", r))
+    r = signed_request(signers[1], 111)
+    r["signature"] = "0OIl" + r["signature"][4:]
+    reqs.append(("bad_base58", r))
+    r = signed_request(signers[1], 112)
+    del r["signature"]
+    reqs.append(("missing_signature", r))
+    reqs.append(("unknown_did", signed_request(unknown, 113, op={"type": "101", "dest": unknown.identifier})))
+    reqs.append(("invalid_verkey", signed_request(bad_vk, 114, op={"type": "101", "x": 1})))
+    reqs.append(("query", signed_request(signers[2], 115, op={"type": "105", "dest": signers[0].identifier})))
+    reqs.append(("no_authenticator", signed_request(signers[2], 116, op={"type": "999"})))
+    reqs.append(("multisig_ok", multi_signed(signers[:3], 117)))
+    reqs.append(("multisig_bad", multi_signed(signers[:3], 118, bad=(1,))))
+    r = signed_request(signers[0], 119)
+    del r["reqId"]
+    reqs.append(("no_reqid", r))
+    r = signed_request(signers[0], 120)
+    r["self"] = 1
+    reqs.append(("bad_kwarg", r))
+    reqs.append(("not_a_dict", [1, 2, 3]))
+    frms = ["cli%d" % (i % 3) for i in range(len(reqs))]
+
+    # client quota: handleOneClientMsg per message, in order, one node
+    ra, core, spy = fresh_authnr()
+    node = _StubNode(methods, metrics_cls, (Batch,), ra)
+    client = []
+    for (label, msg), frm in zip(reqs, frms):
+        node.events.clear()
+        before = spy["calls"]
+        try:
+            node.handleOneClientMsg((json.loads(json.dumps(msg)), frm))
+            raised = None
+        except Exception as ex:
+            raised = {"exc": type(ex).__name__, "msg": str(ex)}
+        client.append({"label": label, "msg": msg, "frm": frm, "events": list(node.events), "raised": raised,
+                       "ids": spy["ids"][-1] if spy["calls"] > before and node.events and
+                       node.events[-1]["ev"] == "accepted" else None,
+                       "authenticate_calls": spy["calls"] - before})
+    # PROPAGATEs of a node Batch: handleOneNodeMsg per message
+    ra, core, spy = fresh_authnr()
+    node = _StubNode(methods, metrics_cls, (Batch,), ra)
+    props = []
+    for j, (label, msg) in enumerate(reqs):
+        if label in ("not_a_dict", "no_reqid", "bad_kwarg"):
+            continue
+        frm = ["Node2", "Node3:9702", "Node4"][j % 3]
+        pm = {"op": "PROPAGATE", "request": msg, "senderClient": "client%d" % j}
+        node.events.clear()
+        try:
+            node.handleOneNodeMsg((json.loads(json.dumps(pm)), frm))
+            raised = None
+        except Exception as ex:
+            raised = {"exc": type(ex).__name__, "msg": str(ex)}
+        props.append({"label": label, "msg": pm, "frm": frm, "events": list(node.events), "raised": raised})
+    return {"clients": clients, "client_quota": client, "propagates": props}
+
+
 GENERATORS = {"serializer.json": lambda: gen_serializer(), "didverifier.json": lambda: gen_didverifier(),
               "authn.json": lambda: gen_authn(), "reqauth.json": lambda: gen_reqauth(),
-              "verdicts.json": lambda: gen_verdicts(), "request.json": lambda: gen_request()}
+              "verdicts.json": lambda: gen_verdicts(), "request.json": lambda: gen_request(),
+              "feed.json": lambda: gen_feed()}
 
 if __name__ == "__main__":
     for name in sys.argv[1:] or list(GENERATORS):
