@@ -25,6 +25,7 @@
 #include "btable.h"
 #include "comb.h"
 #include "keycache.h"
+#include "lp25519.h"
 #include "verify_core.h"
 #include "pv_internal.h"
 #include "../../include/plenum_verify.h"
@@ -48,6 +49,9 @@ static constexpr int PV_BLOCK = 256;
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
 static constexpr uint64_t PV_KEYED_MIN = 32768;   // AUTO: smaller chunks skip dedup (Straus only)
+#ifndef PV_LP_CHAIN_MAX
+#define PV_LP_CHAIN_MAX 2048  // comb keys up to which the per-key chain runs limb-parallel (one wave per key)
+#endif
 #ifndef PV_LATENCY_MAX
 #define PV_LATENCY_MAX 4096  // AUTO: batches up to this size take the latency path (pv_latency.hip)
 #endif
@@ -739,8 +743,8 @@ __device__ __forceinline__ void pv_quad_dbl(fe& X, fe& Y, fe& Z, fe& T, const Qu
 
 // Per distinct key, four lanes: libsodium's key checks, -A, and the bases [256^i](-A), i = 0..31.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
-                                                                         Gate gate) {
-    if (!gate.keyed()) return;
+                                                                         Gate gate, uint32_t lp_max) {
+    if (!gate.keyed() || kw.nkeys[PV_SPLIT_COMB_KEYS] <= lp_max) return;  // pv_key_chain_lp_kernel's batch
     // the chain is the batch's critical path and shares SIMDs with the per-request prep kernel:
     // take issue priority over it
     __builtin_amdgcn_s_setprio(3);
@@ -775,6 +779,50 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const ui
             if (j >= 3 && j <= 5) store(i, j - 2);
         }
     }
+}
+
+// Limb-parallel key chain (lp25519.h): ONE wave per key, every field element over a 16-lane row and
+// the four squarings / products of a doubling in the four rows at once, so the 254 dependent
+// doublings take ~4x less time than on a quad of lanes. Used when the batch has at most `lp_max`
+// comb keys (the wave-per-key kernel fills the chip at ~1,000 keys; beyond that the quad kernel's
+// four lanes per key are the cheaper way to cover many keys); otherwise it exits at once and
+// pv_key_chain_quad_kernel runs. Same outputs: key_flag and the bases [256^i](-A) with their
+// [16], [32], [64] multiples, each carried to reduced limbs before the store.
+__global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __restrict__ pk, KeyWork kw, Gate gate,
+                                                              uint32_t lp_max) {
+#if LP_DEVICE
+    if (!gate.keyed()) return;
+    const uint32_t nk = kw.nkeys[PV_SPLIT_COMB_KEYS];
+    const uint32_t id = blockIdx.x;
+    if (nk > lp_max || id >= nk) return;
+    __builtin_amdgcn_s_setprio(3);
+    uint32_t A[8];
+    pv_load_pk(A, pk, kw.key_owner[kw.comb_key[id]]);
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    lu sw[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) sw[q] = A[q];
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    const bool ok = pv_ge_is_canonical(A) && !pv_has_small_order(A) && dec.ok_a;
+    if (threadIdx.x == 0) kw.key_flag[id] = ok ? 1u : 0u;
+    uint32_t* b = reinterpret_cast<uint32_t*>(kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10);
+    const uint32_t w = 10u * (threadIdx.x >> 4) + (threadIdx.x & 15u);  // word of [X, Y, Z, T] x 10 limbs
+    const bool limb = (threadIdx.x & 15u) < 10u;
+    auto store = [&](int i, int m, const lu& P) {
+        const lu R = lp_carry1(c, P);  // LR -> limb < 2^w + 19: the per-lane code's reduced bound
+        if (limb) b[(i * PV_COMB_PTS + m) * 40 + w] = R;
+    };
+    lu P = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
+    for (int i = 0; i < PV_COMB_POS; i++) {
+        store(i, 0, P);
+        const int nd = i + 1 < PV_COMB_POS ? 8 : 6;
+        for (int j = 0; j < nd; j++) {
+            P = lp_dbl(c, P);
+            if (j >= 3 && j <= 5) store(i, j - 2, P);
+        }
+    }
+#endif
 }
 
 // Per (key, position, block of 16 entries): the comb table rows. Grid-stride over nkeys * 256 items.
@@ -1219,8 +1267,12 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipEventRecord(g_ctx.ev_keys_ready, stream), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(g_ctx.kstream, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
 #if PV_CHAIN_QUAD
+            // one of the two chain kernels runs, by the key count the dedup found (device-side gate)
+            hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(PV_LP_CHAIN_MAX), dim3(64), 0, g_ctx.kstream,
+                               d_pk + 32 * c0, kw, gate, (uint32_t)PV_LP_CHAIN_MAX);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK),
-                               0, g_ctx.kstream, d_pk + 32 * c0, kw, gate);
+                               0, g_ctx.kstream, d_pk + 32 * c0, kw, gate, (uint32_t)PV_LP_CHAIN_MAX);
 #else
             hipLaunchKernelGGL(pv_key_chain_kernel, dim3((limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
                                g_ctx.kstream, d_pk + 32 * c0, kw, gate);
@@ -1714,8 +1766,12 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
         PV_HIP(hipMemcpyAsync(k.d_put_slot, bslot.data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, 12, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         const Gate gate{kw.nkeys, kw.slot_req};
-        hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * m + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0, s,
-                           k.d_put_pk, kw, gate);
+        if (m <= PV_LP_CHAIN_MAX)
+            hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(m), dim3(64), 0, s, k.d_put_pk, kw, gate,
+                               (uint32_t)PV_LP_CHAIN_MAX);
+        else
+            hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * m + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
+                               s, k.d_put_pk, kw, gate, (uint32_t)PV_LP_CHAIN_MAX);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         const uint64_t items = (uint64_t)m * PV_COMB_POS * PV_COMB_BLOCKS;
         hipLaunchKernelGGL(pv_key_fill_kernel, dim3((unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096)),

@@ -302,4 +302,58 @@ int hc_lp_sign_open_cached(const uint8_t* sm, uint64_t smlen, const uint8_t* pk)
     return eq && key_ok && r_ok && sig_ok;
 }
 
+// pv_key_chain_lp_kernel's chain on the host vs pv_comb_chain (the quad / per-lane chain): every
+// stored base equal as a point (affine x, y canonical) and every limb reduced. Returns the number of
+// mismatching bases (0 = identical), or -1 if the key does not decompress.
+int hc_lp_chain_check(const uint8_t* pk) {
+    uint32_t A[8];
+    memcpy(A, pk, 32);
+    ge_p3 negA;
+    if (!pv_key_ok_negate(negA, A)) return -1;
+    std::vector<ge_p3> ref(PV_COMB_POS * PV_COMB_PTS);
+    pv_comb_chain(HostBases{ref.data()}, negA);
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    lu sw[8];
+    for (int q = 0; q < 8; q++) sw[q] = A[q];
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    auto affine = [](const fe& X, const fe& Y, const fe& Z, uint32_t out[16]) {
+        fe zi, x, y;
+        fe_invert(zi, Z);
+        fe_mul(x, X, zi);
+        fe_mul(y, Y, zi);
+        fe_tobytes32(out, x);
+        fe_tobytes32(out + 8, y);
+    };
+    int bad = 0;
+    auto cmp = [&](int i, int m, const lu& P) {
+        const lu R = lp_carry1(c, P);
+        fe X = lp_row_fe(R, 0), Y = lp_row_fe(R, 1), Z = lp_row_fe(R, 2), T = lp_row_fe(R, 3);
+        for (const fe* f : {&X, &Y, &Z, &T}) fe_check_reduced(*f);
+        uint32_t a[16], b[16];
+        affine(X, Y, Z, a);
+        const ge_p3& r = ref[i * PV_COMB_PTS + m];
+        affine(r.X, r.Y, r.Z, b);
+        if (memcmp(a, b, sizeof a)) bad++;
+        // T consistent: X Y == T Z
+        fe xy, tz;
+        fe_mul(xy, X, Y);
+        fe_mul(tz, T, Z);
+        uint32_t u[8], v[8];
+        fe_tobytes32(u, xy);
+        fe_tobytes32(v, tz);
+        if (memcmp(u, v, sizeof u)) bad++;
+    };
+    lu P = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
+    for (int i = 0; i < PV_COMB_POS; i++) {
+        cmp(i, 0, P);
+        const int nd = i + 1 < PV_COMB_POS ? 8 : 6;
+        for (int j = 0; j < nd; j++) {
+            P = lp_dbl(c, P);
+            if (j >= 3 && j <= 5) cmp(i, j - 2, P);
+        }
+    }
+    return bad;
+}
+
 }  // extern "C"

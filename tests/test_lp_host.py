@@ -155,3 +155,14 @@ def test_lp_cached_key_path_golden_verdicts(hc):
         for c in cs[:2]:
             sm, pk = bytes.fromhex(c["sm"]), bytes.fromhex(c["pk"])
             assert bool(hc.hc_lp_sign_open_cached(sm, ctypes.c_uint64(len(sm)), pk)) == c["ok"], key
+
+
+def test_lp_key_chain_matches_per_lane_chain(hc, oracle):
+    """pv_key_chain_lp_kernel's chain (lp doublings, then a carry to reduced limbs) stores the same
+    bases [256^i](-A), [16], [32], [64] multiples as the per-lane chain the fill kernel was built on."""
+    rng = random.Random(8)
+    from vectors import ORDER8
+    keys = [oracle.scalarmult_base(rng.randrange(1, L).to_bytes(32, "little")) for _ in range(3)]
+    keys.append(oracle.point_add(keys[0], ORDER8))  # mixed-order key
+    for pk in keys:
+        assert hc.hc_lp_chain_check(pk) == 0
