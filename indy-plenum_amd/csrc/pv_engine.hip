@@ -31,8 +31,10 @@
 #include "../../include/plenum_verify.h"
 
 static constexpr int PV_BLOCK = 256;
-#ifndef PV_CHAIN_QUAD
-#define PV_CHAIN_QUAD 1  // four lanes per key in the per-key chain (pv_key_chain_quad_kernel)
+#ifndef PV_CHAIN_MODE
+// per-key chain kernel: 2 = limb-parallel, one wave per key (pv_key_chain_lp_kernel); 1 = four lanes
+// per key (pv_key_chain_quad_kernel, round 1); 0 = one lane per key (pv_key_chain_kernel)
+#define PV_CHAIN_MODE 2
 #endif
 #ifndef PV_COMB_A_MINBLOCKS
 #define PV_COMB_A_MINBLOCKS 3
@@ -49,8 +51,8 @@ static constexpr int PV_BLOCK = 256;
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
 static constexpr uint64_t PV_KEYED_MIN = 32768;   // AUTO: smaller chunks skip dedup (Straus only)
-#ifndef PV_LP_CHAIN_MAX
-#define PV_LP_CHAIN_MAX 2048  // comb keys up to which the per-key chain runs limb-parallel (one wave per key)
+#ifndef PV_LP_CHAIN_BLOCKS
+#define PV_LP_CHAIN_BLOCKS 2048  // waves of the limb-parallel key chain (one key each at a time)
 #endif
 #ifndef PV_LATENCY_MAX
 #define PV_LATENCY_MAX 4096  // AUTO: batches up to this size take the latency path (pv_latency.hip)
@@ -743,8 +745,8 @@ __device__ __forceinline__ void pv_quad_dbl(fe& X, fe& Y, fe& Z, fe& T, const Qu
 
 // Per distinct key, four lanes: libsodium's key checks, -A, and the bases [256^i](-A), i = 0..31.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
-                                                                         Gate gate, uint32_t lp_max) {
-    if (!gate.keyed() || kw.nkeys[PV_SPLIT_COMB_KEYS] <= lp_max) return;  // pv_key_chain_lp_kernel's batch
+                                                                         Gate gate) {
+    if (!gate.keyed()) return;
     // the chain is the batch's critical path and shares SIMDs with the per-request prep kernel:
     // take issue priority over it
     __builtin_amdgcn_s_setprio(3);
@@ -781,25 +783,11 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const ui
     }
 }
 
-// Limb-parallel key chain (lp25519.h): ONE wave per key, every field element over a 16-lane row and
-// the four squarings / products of a doubling in the four rows at once, so the 254 dependent
-// doublings take ~4x less time than on a quad of lanes. Used when the batch has at most `lp_max`
-// comb keys (the wave-per-key kernel fills the chip at ~1,000 keys; beyond that the quad kernel's
-// four lanes per key are the cheaper way to cover many keys); otherwise it exits at once and
-// pv_key_chain_quad_kernel runs. Same outputs: key_flag and the bases [256^i](-A) with their
-// [16], [32], [64] multiples, each carried to reduced limbs before the store.
-__global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __restrict__ pk, KeyWork kw, Gate gate,
-                                                              uint32_t lp_max) {
 #if LP_DEVICE
-    if (!gate.keyed()) return;
-    const uint32_t nk = kw.nkeys[PV_SPLIT_COMB_KEYS];
-    const uint32_t id = blockIdx.x;
-    if (nk > lp_max || id >= nk) return;
-    __builtin_amdgcn_s_setprio(3);
+__device__ __forceinline__ void pv_key_chain_lp(const uint8_t* __restrict__ pk, const KeyWork& kw, uint32_t id,
+                                                const LpLane& c, const LpConsts& K) {
     uint32_t A[8];
     pv_load_pk(A, pk, kw.key_owner[kw.comb_key[id]]);
-    const LpLane c = LpLane::make();
-    const LpConsts K = LpConsts::make(c);
     lu sw[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) sw[q] = A[q];
@@ -822,6 +810,26 @@ __global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __re
             if (j >= 3 && j <= 5) store(i, j - 2, P);
         }
     }
+}
+#endif
+
+// Limb-parallel key chain (lp25519.h): ONE wave per key, every field element over a 16-lane row and
+// the four squarings / products of a doubling in the four rows at once, so the 254 dependent
+// doublings take ~4x less time than on a quad of lanes. Blocks stride over the keys (a batch with
+// more keys than blocks runs them in turn), so the launch needs no host-side key count and no gated
+// companion kernel: a gated launch is not free on a saturated chip, its blocks wait ~0.2 ms for
+// dispatch slots (rocprofv3, profiles/r02/prof_a). Same outputs as pv_key_chain_quad_kernel: key_flag
+// and the bases [256^i](-A) with their [16], [32], [64] multiples, carried to reduced limbs.
+__global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __restrict__ pk, KeyWork kw, Gate gate) {
+#if LP_DEVICE
+    if (!gate.keyed()) return;
+    const uint32_t nk = kw.nkeys[PV_SPLIT_COMB_KEYS];
+    if (blockIdx.x >= nk) return;
+    __builtin_amdgcn_s_setprio(3);
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    for (uint32_t id = blockIdx.x; id < nk; id += gridDim.x)
+        pv_key_chain_lp(pk, kw, id, c, K);
 #endif
 }
 
@@ -1266,13 +1274,12 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             // overlapped with the per-request prep on the main stream
             PV_HIP(hipEventRecord(g_ctx.ev_keys_ready, stream), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(g_ctx.kstream, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
-#if PV_CHAIN_QUAD
-            // one of the two chain kernels runs, by the key count the dedup found (device-side gate)
-            hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(PV_LP_CHAIN_MAX), dim3(64), 0, g_ctx.kstream,
-                               d_pk + 32 * c0, kw, gate, (uint32_t)PV_LP_CHAIN_MAX);
-            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#if PV_CHAIN_MODE == 2
+            hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(limit, PV_LP_CHAIN_BLOCKS)), dim3(64), 0,
+                               g_ctx.kstream, d_pk + 32 * c0, kw, gate);
+#elif PV_CHAIN_MODE == 1
             hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK),
-                               0, g_ctx.kstream, d_pk + 32 * c0, kw, gate, (uint32_t)PV_LP_CHAIN_MAX);
+                               0, g_ctx.kstream, d_pk + 32 * c0, kw, gate);
 #else
             hipLaunchKernelGGL(pv_key_chain_kernel, dim3((limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
                                g_ctx.kstream, d_pk + 32 * c0, kw, gate);
@@ -1766,12 +1773,8 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
         PV_HIP(hipMemcpyAsync(k.d_put_slot, bslot.data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, 12, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         const Gate gate{kw.nkeys, kw.slot_req};
-        if (m <= PV_LP_CHAIN_MAX)
-            hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(m), dim3(64), 0, s, k.d_put_pk, kw, gate,
-                               (uint32_t)PV_LP_CHAIN_MAX);
-        else
-            hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * m + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
-                               s, k.d_put_pk, kw, gate, (uint32_t)PV_LP_CHAIN_MAX);
+        hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(m, PV_LP_CHAIN_BLOCKS)), dim3(64), 0, s,
+                           k.d_put_pk, kw, gate);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         const uint64_t items = (uint64_t)m * PV_COMB_POS * PV_COMB_BLOCKS;
         hipLaunchKernelGGL(pv_key_fill_kernel, dim3((unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096)),
