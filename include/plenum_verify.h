@@ -248,6 +248,63 @@ int pv_signing_serialize_json(const char* json, const uint64_t* off, uint64_t n,
                               int threads, uint8_t* msg_out, uint64_t msg_cap, uint64_t* msg_off, uint8_t* digest,
                               uint8_t* status);
 
+/* Fused ingress planning (replaces the per-request Python planning of the wire
+ * path: json.loads -> Request(**msg).as_dict -> CoreAuthMixin._select_signatures,
+ * plenum/server/client_authn.py:240-264, node.py:1643,2636-2650). ONE parse of every received
+ * request gives what pv_signing_serialize_json(PV_SER_REQUEST) gives (msg, msg_off, digest, status)
+ * and its signature plan:
+ *   kind[i]  PV_PLAN_SINGLE  {identifier: signature}: both non-empty strings (the first branch of
+ *                            _select_signatures)
+ *            PV_PLAN_MULTI   the `signatures` object (non-empty, string values, no duplicate
+ *                            names) of a request without a usable identifier/signature pair and
+ *                            without a `signature` value (so the verified-request cache stores None)
+ *            PV_PLAN_PY      anything else: the caller runs the reference's Python path for it
+ *                            (serialization status not OK, not an object, a `self` key, plugin
+ *                            fields registered, operation not an object or its type not a string,
+ *                            non-ASCII or escaped identifier/signature text, trailing whitespace, ...)
+ *   type_id[i]      operation["type"] of a SINGLE/MULTI request, as an index into the distinct type
+ *                   strings types[type_off[t] : type_off[t+1]] (first-appearance order)
+ *   pair_off[i]     request i's (identifier, signature) pairs are [pair_off[i], pair_off[i+1])
+ *                   (dict order); pair_name[p] indexes the distinct identifier strings
+ *                   names[name_off[k] : name_off[k+1]]; sigs[sig_off[p] : sig_off[p+1]] is the
+ *                   signature text (ASCII)
+ * Capacities: msg_cap as pv_signing_serialize_json; sigs_cap, names_cap and types_cap are byte
+ * capacities and off[n] always suffices (every string is a substring of its request); pair_cap =
+ * off[n] / 6 + 1 always suffices (a pair takes at least 6 bytes of JSON). name_off holds
+ * pair_cap + 1 entries (distinct names <= pairs), type_off n + 1 (distinct types <= requests).
+ * Returns PV_ERR_ARG with msg_off[n] = bytes needed when msg_cap is too small. */
+#define PV_PLAN_PY 0
+#define PV_PLAN_SINGLE 1
+#define PV_PLAN_MULTI 2
+typedef struct {
+    uint8_t* msg_out; /* in: buffers */
+    uint64_t msg_cap;
+    uint64_t* msg_off;  /* [n + 1] */
+    uint8_t* digest;    /* [32 n] */
+    uint8_t* status;    /* [n] PV_SER_* */
+    uint8_t* kind;      /* [n] PV_PLAN_* */
+    uint32_t* type_id;  /* [n] */
+    uint64_t* pair_off; /* [n + 1] */
+    uint32_t* pair_name; /* [pair_cap] */
+    uint64_t* sig_off;   /* [pair_cap + 1] */
+    uint64_t pair_cap;
+    char* sigs;
+    uint64_t sigs_cap;
+    char* names;
+    uint64_t* name_off; /* [pair_cap + 1] */
+    uint64_t names_cap;
+    char* types;
+    uint64_t* type_off; /* [n + 1] */
+    uint64_t types_cap;
+    char* keys_hex;   /* [65 n] or NULL: Request.digest of request i as 64 lowercase hex digits + '\n' */
+    char* sig_lines;  /* [sigs_cap + pair_cap] or NULL: every signature text followed by '\n' */
+    uint64_t n_pairs; /* out */
+    uint64_t n_names; /* out */
+    uint64_t n_types; /* out */
+} PvWirePlan;
+int pv_wire_plan(const char* json, const uint64_t* off, uint64_t n, const char* plugin_fields, int threads,
+                 PvWirePlan* plan);
+
 /* Multi-GPU: one process per GPU. pv_comm_unique_id on rank 0, broadcast the 128 bytes by any
  * channel, pv_comm_init on every rank (after pv_init). pv_allgather_verdicts gathers
  * words_per_rank 64-bit verdict words from every rank into d_all (nranks * words_per_rank) with

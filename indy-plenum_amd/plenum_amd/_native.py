@@ -56,6 +56,8 @@ SIGNATURES = {
     "pv_signing_serialize_json": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                                  ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "pv_wire_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_int,
+                                    ctypes.c_void_p]),
     "pv_ingress_front_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double)]),
     "pv_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_comm_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),

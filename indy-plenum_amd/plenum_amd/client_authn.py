@@ -159,6 +159,17 @@ class VerkeyResolver:
         except Exception as ex:
             return LookupError(ex)
 
+    def static(self, idr):
+        """The verkey of ``idr`` when it does not depend on the request (a registry or state
+        record: what getVerkey returns for every request of the batch), else None (request-
+        dependent, or getVerkey would raise: the caller takes the per-request path)."""
+        if not self.batched:
+            return None
+        r = self.memo.get(idr, _MISS)
+        if r is _MISS:
+            r = self.memo[idr] = self._record(idr)
+        return None if r is _PER_REQUEST or isinstance(r, LookupError) else r
+
     def get(self, idr, request):
         if not self.batched:
             try:
