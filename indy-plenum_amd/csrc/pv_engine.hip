@@ -86,15 +86,25 @@ struct Soa {
     }
 };
 
-// Per-lane cached table of [j](-A) in HBM, layout [entry][quad][slot] uint4. Indices are 32-bit
-// (chunk <= 2^20 slots, so (9 * 10 + 9) * 2^20 + slot < 2^32) so each access is a uniform 64-bit base
-// plus one per-lane 32-bit offset instead of ten live 64-bit addresses.
+// Per-lane cached table of [j](-A) in HBM. Indices are 32-bit (chunk <= 2^20 slots, 90 quads per
+// slot < 2^32) so each access is a uniform 64-bit base plus one per-lane 32-bit offset instead of ten
+// live 64-bit addresses. Layout PV_ATAB_AOS = 1: [slot][entry][quad] uint4 -- the lanes of a wave pick
+// different entries (their own digits), so each lane reads its own contiguous 160 B entry (two
+// 128 B lines) instead of a 16 B piece of a line shared with lanes that want other entries
+// ([entry][quad][slot], PV_ATAB_AOS = 0: coalesced only when every lane has the same digit).
+#ifndef PV_ATAB_AOS
+#define PV_ATAB_AOS 1
+#endif
 struct DevATab {
     uint4* base;
     uint32_t nslots;
     uint32_t slot;
     __device__ __forceinline__ uint4& at(int j, int q) const {
+#if PV_ATAB_AOS
+        return base[(slot * 9u + (uint32_t)j) * 10u + (uint32_t)q];
+#else
         return base[(uint32_t)(j * 10 + q) * nslots + slot];
+#endif
     }
     __device__ __forceinline__ void store(int j, const uint32_t w[40]) const {
 #pragma unroll
