@@ -90,6 +90,56 @@ PV_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
 #endif
 }
 PV_HD uint64_t mul64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
+// PV_MAD_COLASM: each product-scanning column is ONE inline-asm block of N dependent
+// v_mad_u64_u32 (accumulator in place). The per-mad empty asm of PV_MAD_CHAIN keeps the chain but
+// the hazard recognizer cannot see through inline asm and pads EVERY mad that follows one with an
+// `s_nop 0` (it assumes the asm may have been a transcendental op writing the VGPR: ~100 s_nop per
+// field multiplication). A whole column per block leaves at most one pad per column. Device only.
+#ifndef PV_MAD_COLASM
+#define PV_MAD_COLASM 1
+#endif
+#define PV_MA(a, b) "v_mad_u64_u32 %0, %1, %" #a ", %" #b ", %0\n\t"
+#define PV_M0(a, b) "v_mad_u64_u32 %0, %1, %" #a ", %" #b ", 0\n\t"
+// acc (+)= sum_i a[i] * b[i], N terms; FIRST: acc starts at 0 (the first mad adds the constant 0)
+template <int N, bool FIRST>
+__device__ __forceinline__ void pv_madcol(uint64_t& acc, const uint32_t* a, const uint32_t* b) {
+    uint64_t cc;
+    if constexpr (N == 10 && FIRST) {
+        asm(PV_M0(2, 12) PV_MA(3, 13) PV_MA(4, 14) PV_MA(5, 15) PV_MA(6, 16) PV_MA(7, 17) PV_MA(8, 18)
+                PV_MA(9, 19) PV_MA(10, 20) PV_MA(11, 21)
+            : "=&v"(acc), "=&s"(cc)
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
+              "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]),
+              "v"(b[8]), "v"(b[9]));
+    } else if constexpr (N == 10) {
+        asm(PV_MA(2, 12) PV_MA(3, 13) PV_MA(4, 14) PV_MA(5, 15) PV_MA(6, 16) PV_MA(7, 17) PV_MA(8, 18)
+                PV_MA(9, 19) PV_MA(10, 20) PV_MA(11, 21)
+            : "+v"(acc), "=&s"(cc)
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8]),
+              "v"(a[9]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]),
+              "v"(b[8]), "v"(b[9]));
+    } else if constexpr (N == 6 && FIRST) {
+        asm(PV_M0(2, 8) PV_MA(3, 9) PV_MA(4, 10) PV_MA(5, 11) PV_MA(6, 12) PV_MA(7, 13)
+            : "=&v"(acc), "=&s"(cc)
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(b[0]), "v"(b[1]), "v"(b[2]),
+              "v"(b[3]), "v"(b[4]), "v"(b[5]));
+    } else if constexpr (N == 6) {
+        asm(PV_MA(2, 8) PV_MA(3, 9) PV_MA(4, 10) PV_MA(5, 11) PV_MA(6, 12) PV_MA(7, 13)
+            : "+v"(acc), "=&s"(cc)
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(b[0]), "v"(b[1]), "v"(b[2]),
+              "v"(b[3]), "v"(b[4]), "v"(b[5]));
+    } else if constexpr (N == 5 && !FIRST) {
+        asm(PV_MA(2, 7) PV_MA(3, 8) PV_MA(4, 9) PV_MA(5, 10) PV_MA(6, 11)
+            : "+v"(acc), "=&s"(cc)
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]),
+              "v"(b[4]));
+    } else {
+        static_assert(N == 10 || N == 6 || (N == 5 && !FIRST), "pv_madcol: unsupported column shape");
+    }
+}
+#undef PV_MA
+#undef PV_M0
+
 // Opaque copy: stops the compiler from re-associating a column sum so that the carry from the
 // previous column is added by a separate v_lshl_add_u64 instead of entering the first
 // v_mad_u64_u32 of the column as its accumulator (no instruction is emitted).
@@ -217,6 +267,7 @@ PV_HD void fe_mul_pre(fe& hout, const fe& f, const fe& g, const uint32_t g19[10]
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 10; k++) {
+        uint32_t ca[10], cb[10];
 #pragma unroll
         for (int i = 0; i < 10; i++) {
             const int j = k - i;
@@ -229,9 +280,19 @@ PV_HD void fe_mul_pre(fe& hout, const fe& f, const fe& g, const uint32_t g19[10]
                 b = g19[j + 10];
             }
             PV_COL_TRACK(k, a, b);
-            acc = (k == 0 && i == 0) ? mul64(a, b) : mad64(a, b, acc);
+            ca[i] = a;
+            cb[i] = b;
+        }
+#if defined(__HIP_DEVICE_COMPILE__) && PV_MAD_COLASM
+        if (k == 0) pv_madcol<10, true>(acc, ca, cb);
+        else pv_madcol<10, false>(acc, ca, cb);
+#else
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            acc = (k == 0 && i == 0) ? mul64(ca[i], cb[i]) : mad64(ca[i], cb[i], acc);
             if (i == 0 && k > 0) acc = pv_opaque64(acc);
         }
+#endif
 #ifdef PV_BOUNDS_CHECK
         if (k > 0) col128[k] += col128[k - 1] >> ((k & 1) ? 26 : 25);
         PV_ASSERT((col128[k] >> 64) == 0, "mul column overflow");
@@ -269,7 +330,8 @@ PV_HD void fe_sq(fe& hout, const fe& f) {
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 10; k++) {
-        bool first = true;
+        uint32_t ca[6], cb[6];
+        int nt = 0;
 #pragma unroll
         for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -281,11 +343,23 @@ PV_HD void fe_sq(fe& hout, const fe& f) {
                 const uint32_t a = (c == 1) ? f.v[i] : (c == 2 ? f2[i] : f4[i]);
                 const uint32_t b = wrap ? f19[j] : f.v[j];
                 PV_COL_TRACK(k, a, b);
-                acc = (k == 0 && first) ? mul64(a, b) : mad64(a, b, acc);
-                if (first && k > 0) acc = pv_opaque64(acc);
-                first = false;
+                ca[nt] = a;
+                cb[nt] = b;
+                nt++;
             }
         }
+        // even columns have 6 terms, odd columns 5
+#if defined(__HIP_DEVICE_COMPILE__) && PV_MAD_COLASM
+        if (k == 0) pv_madcol<6, true>(acc, ca, cb);
+        else if (k & 1) pv_madcol<5, false>(acc, ca, cb);
+        else pv_madcol<6, false>(acc, ca, cb);
+#else
+#pragma unroll
+        for (int t = 0; t < 6 - (k & 1); t++) {
+            acc = (k == 0 && t == 0) ? mul64(ca[t], cb[t]) : mad64(ca[t], cb[t], acc);
+            if (t == 0 && k > 0) acc = pv_opaque64(acc);
+        }
+#endif
 #ifdef PV_BOUNDS_CHECK
         if (k > 0) col128[k] += col128[k - 1] >> ((k & 1) ? 26 : 25);
         PV_ASSERT((col128[k] >> 64) == 0, "sq column overflow");

@@ -3,7 +3,7 @@
 #   microbench/build_variants.sh NAME "-DFLAG=.. ..." [NAME "FLAGS" ...]  -> microbench/variants/NAME.so
 # Load one with PLENUM_AMD_LIB=microbench/variants/NAME.so (tests/perf_quick.py, bench.py).
 cd "$(dirname "$0")/../indy-plenum_amd" || exit 1
-SRC="csrc/pv_engine.hip csrc/pv_ingress.hip csrc/host_prep.cpp csrc/signing_json.cpp"
+SRC="csrc/pv_engine.hip csrc/pv_latency.hip csrc/pv_ingress.hip csrc/host_prep.cpp csrc/signing_json.cpp"
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
