@@ -10,6 +10,7 @@ instances, averaged over dispatches, plus derived figures):
   hbm_read_bytes_x2 = 2 x that                   MI355X_MICROARCH.md: FETCH_SIZE reads 1/2 of the
                                                   bytes of a wide coalesced 16-B/lane stream on gfx950
   hbm_write_bytes = WRITE_SIZE (KiB) * 1024
+  hbm_bytes_per_launch_corrected = hbm_read_bytes_x2 + hbm_write_bytes   (bench roofline.traffic)
   eff_clock_GHz   = GRBM_GUI_ACTIVE / 8 XCDs / dispatch seconds
   valu_instr_per_request = SQ_INSTS_VALU * 64 / requests   (wave-instructions x 64 lanes)
 A dispatch shorter than GATED_NS is a launch the device-side path gate turned into a no-op.
@@ -65,7 +66,11 @@ def pmc(dbs):
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    argv = sys.argv[1:]
+    if "--requests" in argv:  # drop the option and its value
+        i = argv.index("--requests")
+        argv = argv[:i] + argv[i + 2:]
+    args = [a for a in argv if not a.startswith("--")]
     requests = 1 << 20
     if "--requests" in sys.argv:
         requests = int(sys.argv[sys.argv.index("--requests") + 1])
@@ -94,6 +99,9 @@ def main():
             d["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
         if "hbm_read_bytes" in d and "hbm_write_bytes" in d:
             d["hbm_bytes_per_launch"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
+            # the guide's gfx950 correction (FETCH_SIZE x 2 for 16-B/lane streaming reads) + writes:
+            # the figure the bench line reports as roofline.traffic
+            d["hbm_bytes_per_launch_corrected"] = d["hbm_read_bytes_x2"] + d["hbm_write_bytes"]
             d["hbm_bytes_per_request"] = d["hbm_bytes_per_launch"] / requests
         if "GRBM_GUI_ACTIVE" in avg and secs:
             d["eff_clock_GHz"] = avg["GRBM_GUI_ACTIVE"] / 8 / secs / 1e9
