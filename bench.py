@@ -597,7 +597,8 @@ def main():
                      "achieved": round(achieved / 1e12, 3), "peak": round(BC.PEAK_MAC_PER_S / 1e12, 3),
                      "unit": "TMAC/s (v_mad_u64_u32 int32 MACs)", "frac": round(achieved / BC.PEAK_MAC_PER_S, 4),
                      "traffic": pmc_traffic("pv_comb_a_kernel" if comb else "pv_msm_kernel"),
-                     "algorithmic_mac_per_verify": round(mac_kernel), "launch_ms": round(launch_ms, 4)},
+                     "algorithmic_mac_per_verify": round(mac_kernel), "launch_ms": round(launch_ms, 4),
+                     "frac_of_measured_mad_stream": round(achieved / BC.MEASURED_MAD_STREAM_MAC_PER_S, 4)},
         "pipeline": {**{s + "_ms": round(v, 4) for s, v in stage_ms.items()},
                      "kernel_verifies_per_s_per_gpu": round(per_gpu_rate, 1),
                      "whole_pipeline_valu_frac": round(mac_executed * per_gpu_rate / BC.PEAK_MAC_PER_S, 4),

@@ -61,6 +61,10 @@ MAC_COMB_PER_KEY = _mac(_S_DECOMP, _M_DECOMP) + _mac(31 * 8 * 4, 31 * (8 * 3 + 1
 # full-rate v_add_u32 time there); 256 CU x 4 SIMD x 64 lanes / 4 cycles x 2.4 GHz.
 CUS, SIMDS, LANES, CLOCK_HZ, MAD64_CYCLES = 256, 4, 64, 2.4e9, 4
 PEAK_MAC_PER_S = CUS * SIMDS * LANES * CLOCK_HZ / MAD64_CYCLES  # 3.93e13
+# What a pure stream of independent v_mad_u64_u32 actually sustains on the chip (clock under load,
+# issue): profiles/r01_isa_rates_full.jsonl, 4 waves/SIMD = 4.987e11 wave-instructions/s x 64 lanes.
+# Reported beside the nominal peak, never in place of it.
+MEASURED_MAD_STREAM_MAC_PER_S = 4.987e11 * 64  # 3.19e13
 
 # Bytes a verification needs from HBM at minimum: the record (64 B signature + ~299 B message)
 # + 32 B key + 8 B offset; the verdict bit is negligible.

@@ -189,6 +189,43 @@ PV_HD void pv_comb_b_acc_staged(ge_p3& acc, const BStage& st, const Dig& dig) {
     }
 }
 
+// One cached addition of the staged entry (sign `neg`) to acc; unless LAST, starts the fetch of
+// position i - 1's entry (digit from ew, reloaded every 4 positions) between the products.
+template <bool LAST, class AStage, class Dig>
+PV_HD void pv_comb_a_step(ge_p1p1& t, const ge_p3& acc, const AStage& st, const Dig& dig, int i, uint32_t& ew,
+                          int& e) {
+    const bool neg = e < 0;
+    uint32_t w[20];
+    st.staged(0, w);
+    fe ypx, ymx, tt, a, b, c, d, z2, t2d;
+    pv_sel_pm(ypx, ymx, w, neg);
+    if (!LAST && (i & 3) == 0) ew = dig.ek((i - 1) >> 2);  // lands during the two products
+    fe_sub(tt, acc.Y, acc.X);
+    fe_mul(a, tt, ymx);
+    fe_add(tt, acc.Y, acc.X);
+    fe_mul(b, tt, ypx);
+    st.staged(1, w);
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        z2.v[q] = w[q];
+        t2d.v[q] = w[10 + q];
+    }
+    if (!LAST) {
+        e = pv_byte(ew, i - 1);
+        st.stage(i - 1, e < 0 ? -e : e);
+    }
+    fe_cneg(t2d, t2d, neg);
+    fe_mul(c, acc.T, t2d);
+    fe_mul(d, acc.Z, z2);
+    fe_sub(t.X, b, a);
+    fe_add(t.Y, b, a);
+    fe_add(t.Z, d, c);
+    fe_sub(t.T, d, c);
+}
+
+// Positions 31..1 in the loop (extended result, next fetch always started), position 0 peeled: the
+// loop body then has no p3/p2 merge (whose phi copies cost ~30 v_mov per addition) and no
+// last-iteration branches.
 template <class AStage, class Dig>
 PV_HD void pv_comb_a_xyz_staged(fe& X, fe& Y, fe& Z, const ge_p3& accB, const AStage& st, const Dig& dig) {
     ge_p3 acc = accB;
@@ -196,40 +233,12 @@ PV_HD void pv_comb_a_xyz_staged(fe& X, fe& Y, fe& Z, const ge_p3& accB, const AS
     uint32_t ew = dig.ek(7);
     int e = pv_byte(ew, PV_COMB_POS - 1);
     st.stage(PV_COMB_POS - 1, e < 0 ? -e : e);
-    for (int i = PV_COMB_POS - 1; i >= 0; i--) {
-        const bool neg = e < 0;
-        uint32_t w[20];
-        st.staged(0, w);
-        fe ypx, ymx, tt, a, b, c, d, z2, t2d;
-        pv_sel_pm(ypx, ymx, w, neg);
-        if (i > 0 && (i & 3) == 0) ew = dig.ek((i - 1) >> 2);  // lands during the two products
-        fe_sub(tt, acc.Y, acc.X);
-        fe_mul(a, tt, ymx);
-        fe_add(tt, acc.Y, acc.X);
-        fe_mul(b, tt, ypx);
-        st.staged(1, w);
-#pragma unroll
-        for (int q = 0; q < 10; q++) {
-            z2.v[q] = w[q];
-            t2d.v[q] = w[10 + q];
-        }
-        if (i > 0) {
-            e = pv_byte(ew, i - 1);
-            st.stage(i - 1, e < 0 ? -e : e);
-        }
-        fe_cneg(t2d, t2d, neg);
-        fe_mul(c, acc.T, t2d);
-        fe_mul(d, acc.Z, z2);
-        fe_sub(t.X, b, a);
-        fe_add(t.Y, b, a);
-        fe_add(t.Z, d, c);
-        fe_sub(t.T, d, c);
-        if (i > 0) {
-            ge_p1p1_to_p3(acc, t);
-        } else {
-            ge_p1p1_to_p2(X, Y, Z, t);
-        }
+    for (int i = PV_COMB_POS - 1; i >= 1; i--) {
+        pv_comb_a_step<false>(t, acc, st, dig, i, ew, e);
+        ge_p1p1_to_p3(acc, t);
     }
+    pv_comb_a_step<true>(t, acc, st, dig, 0, ew, e);
+    ge_p1p1_to_p2(X, Y, Z, t);
 }
 
 // Staging over plain Rows objects (host tests): stage() remembers the entry, staged() reads it.

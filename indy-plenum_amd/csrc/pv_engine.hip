@@ -629,6 +629,18 @@ __device__ __forceinline__ void pv_glds16(const uint4* g, uint4* l) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                      (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
+// Q pieces of 16 B from g[0..Q) to l[q * 64 + lane] (a wave's [q][lane] staging area). The
+// instruction's immediate offset (16 q) applies to BOTH the global and the LDS address, so the LDS
+// base of piece q is moved back by the same 16 q bytes (M0 is set per instruction anyway): all Q
+// loads then share ONE 64-bit global address instead of Q 64-bit adds per staged entry.
+template <int Q, int q = 0>
+__device__ __forceinline__ void pv_glds16_row(const uint4* g, uint4* l) {
+    if constexpr (q < Q) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)(l + q * 64 - q), 16, 16 * q, 0);
+        pv_glds16_row<Q, q + 1>(g, l);
+    }
+}
 // the LDS reads of the previous staged entry must be complete before its buffer is refilled
 __device__ __forceinline__ void pv_lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -639,8 +651,7 @@ struct DevCombStage {  // per-key comb table rows, entries of 10 uint4
     __device__ __forceinline__ void stage(int i, int d) const {
         const uint4* e = key + ((uint32_t)i * PV_COMB_ENT + (uint32_t)d) * 10;
         pv_lds_reads_done();
-#pragma unroll
-        for (int q = 0; q < 10; q++) pv_glds16(e + q, lds + q * 64);
+        pv_glds16_row<10>(e, lds);
     }
     __device__ __forceinline__ void staged(int h, uint32_t w[20]) const {
 #pragma unroll
@@ -660,8 +671,7 @@ struct DevBStage {  // fixed-base comb rows, entries of PV_BCOMB_STRIDE words (8
     __device__ __forceinline__ void stage(int j, int d) const {
         const uint4* e = base + ((uint32_t)j * PV_BCOMB_ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4);
         pv_lds_reads_done();
-#pragma unroll
-        for (int q = 0; q < PV_BCOMB_STRIDE / 4; q++) pv_glds16(e + q, lds + q * 64);
+        pv_glds16_row<PV_BCOMB_STRIDE / 4>(e, lds);
     }
     __device__ __forceinline__ void staged(int part, uint32_t w[20]) const {
 #pragma unroll
