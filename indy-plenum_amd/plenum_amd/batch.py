@@ -73,12 +73,28 @@ def _stack():
 
 
 @contextmanager
-def active(cache, engine=None):
-    _stack().append((cache, engine))
+def active(cache, engine=None, answers=None):
+    """Run per-request logic against a batch's verdicts. ``answers`` (optional): {id(req_data):
+    (req_data, authenticator, identifiers)} for requests whose whole authenticate() outcome the
+    batch already knows (the wire plan's device-finished requests)."""
+    _stack().append((cache, engine, answers))
     try:
         yield cache
     finally:
         _stack().pop()
+
+
+def answer(authnr, req_data):
+    """The identifiers ``authnr.authenticate(req_data)`` returns, when the active batch computed
+    them for this very request object and authenticator (every signature verified on the device,
+    signers resolved exactly as authenticate resolves them); else None."""
+    s = _stack()
+    if not s or not s[-1][2]:
+        return None
+    a = s[-1][2].get(id(req_data))
+    if a is None or a[0] is not req_data or a[1] is not authnr:
+        return None
+    return list(a[2])
 
 
 def verdict(pk, sm):
@@ -86,7 +102,7 @@ def verdict(pk, sm):
     s = _stack()
     engine = None
     if s:
-        cache, engine = s[-1]
+        cache, engine, _ = s[-1]
         v = cache.get(pk, sm)
         if v is not None:
             return v

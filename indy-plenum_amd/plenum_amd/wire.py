@@ -343,10 +343,12 @@ _MISSING = object()
 def _fast_capable(core, one_call_per_request):
     """The device may finish a request for `core` only where pv_wire_plan reproduces its Python
     planning: CoreAuthMixin's signature selection and signing view, batched verkey lookup."""
-    if one_call_per_request or core is None or not hasattr(core, "plan_verifications"):
+    if core is None or not hasattr(core, "plan_verifications"):
         return None
     from .client_authn import CoreAuthMixin
     cls = type(core)
+    if one_call_per_request and getattr(cls, "authenticate", None) is not CoreAuthMixin.authenticate:
+        return None  # only CoreAuthMixin.authenticate takes the batch's precomputed answer
     if (getattr(cls, "_select_signatures", None) is not CoreAuthMixin._select_signatures
             or getattr(cls, "_signing_view", None) is not CoreAuthMixin._signing_view
             or set(getattr(core, "excluded_from_signing", ())) != _EXCLUDED):
@@ -431,6 +433,28 @@ def _authenticate_packed(req_authnr, blob, off, threads, timings, one_call_per_r
     keys_all = P.keys()  # request i's key (Request.digest, hex) when its serialization succeeded
     ser_ok = (P.status == PV_SER_OK).tolist()
     msgs, other, slow_views = {}, {}, []
+    names = P.names
+    pn, po = P.pair_name, P.pair_off
+    answers = {}
+    if one_call_per_request and fast.any():
+        # the reference's call pattern: every request still goes through req_authnr.authenticate
+        # once, with the request dict it would get; for a device-finished request the core
+        # authenticator answers from the plan (identifiers in signature-dict order) instead of
+        # re-serializing and re-resolving every signer
+        for i in np.nonzero(fast)[0].tolist():
+            msg = None
+            try:
+                msg = _loads(blob[int(off[i]):int(off[i + 1])].tobytes())
+                view = _request_view(msg)
+                if view is None:
+                    view = Request(**msg).as_dict
+            except Exception as ex:
+                msgs[i] = msg
+                other[i] = (_FAILED, None, ex)
+                continue
+            msgs[i] = msg
+            answers[id(view)] = (view, core, [names[q] for q in pn[int(po[i]):int(po[i + 1])].tolist()])
+            other[i] = (_SLOW, view, keys_all[i])
     for i in np.nonzero(~fast)[0].tolist():  # decoded and classified as the sequential path does
         msg = None
         try:
@@ -458,11 +482,11 @@ def _authenticate_packed(req_authnr, blob, off, threads, timings, one_call_per_r
     cache = batch.VerdictCache()
     if slow_views and core is not None and hasattr(core, "plan_verifications"):
         cache.fill(core.plan_verifications(slow_views))
+    if one_call_per_request:
+        fast[:] = False  # every request takes one authenticate call
     results = [None] * n
     verified = req_authnr._verified_reqs
     vget = verified.get
-    names = P.names
-    pn, po = P.pair_name, P.pair_off
     kind = P.kind
     sigs_all = P.signatures() if fast.any() else []
 
@@ -512,7 +536,7 @@ def _authenticate_packed(req_authnr, blob, off, threads, timings, one_call_per_r
         verified.update(zip(keys, [{'signature': s, 'identifiers': d} for s, d in zip(sigs_all[p0:p1], ids)]))
         results[a:b] = ids
 
-    with batch.active(cache):
+    with batch.active(cache, answers=answers):
         start = 0
         for j in np.nonzero(~simple)[0].tolist() + [n]:
             if j > start:

@@ -8,7 +8,7 @@ import json
 import numpy as np
 import pytest
 
-from plenum_amd import _native
+from plenum_amd import _native, batch
 from plenum_amd.base58 import b58decode
 from plenum_amd.client_authn import CoreAuthNr, VerkeyResolver
 from plenum_amd.state_utils import DictState
@@ -191,7 +191,7 @@ def test_loads_matches_json_loads(raw):
         assert a == b
 
 
-def test_wire_batch_one_call_per_request_cpu(cpu_engine, sodium):
+def test_wire_batch_one_call_per_request_cpu(cpu_engine, sodium, monkeypatch):
     """one_call_per_request=True: the reference's call pattern (ReqAuthenticator.authenticate ->
     CoreAuthNr.authenticate once per request that is not a verified-cache hit; test_no_reauth's
     spy), identical results, every signature check in one launch."""
@@ -212,8 +212,18 @@ def test_wire_batch_one_call_per_request_cpu(cpu_engine, sodium):
     spy(ra_wire, "wire")
     want = [norm(r) for r in sequential(ra_seq, raws)]
     cpu_engine["sm"] = 0
+    answered = []
+    orig_answer = batch.answer
+
+    def answer_spy(authnr, req_data):
+        a = orig_answer(authnr, req_data)
+        answered.append(a is not None)
+        return a
+    monkeypatch.setattr(batch, "answer", answer_spy)
     got = [norm(r) for r in wire.authenticate_wire_batch(ra_wire, raws, one_call_per_request=True)]
     assert got == want
     assert ra_wire._verified_reqs == ra_seq._verified_reqs
     assert counts["wire"] == counts["seq"] > 10
     assert cpu_engine["sm"] == 1  # the plan's one launch; nothing verified one by one
+    # device-finished requests were answered from the plan inside the one authenticate call
+    assert sum(answered) > 10 and not all(answered)
