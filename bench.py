@@ -609,6 +609,33 @@ def main():
         "verdicts_check": "bitmap == known bits (valid except %d tampered records per GPU)%s" % (
             tamper_count(n), ", all %d shards' gathered bitmaps checked on every rank" % world if world > 1 else ""),
     }
+    if world > 1 and not args.no_host_path:
+        # SURVEY.md §8e host traffic: each rank's shard from host buffers (pv_verify_batch: pinned
+        # staging pipelined with the H2D DMA, kernels, verdicts back), on up to configs[4]'s 8M-request
+        # shard; max over ranks. Reported beside the device-resident headline, never as `value`.
+        hs = min(n, CONFIG5_TOTAL // 8)
+        ho = off[:hs + 1]
+        err, hel, hv = None, 0.0, None
+        try:  # a host-side limit must not cost the headline line; every rank still joins each collective
+            _native.verify_sm_batch(blob[:int(ho[-1])], ho, pks[:hs])  # staging buffers sized
+        except Exception as ex:
+            err = ex
+        barrier_sync()
+        if err is None:
+            try:
+                t1 = time.perf_counter()
+                hv = _native.verify_sm_batch(blob[:int(ho[-1])], ho, pks[:hs])
+                hel = time.perf_counter() - t1
+            except Exception as ex:
+                err = ex
+        hel = comm.max_f64(hel if err is None else 1e30)
+        if hel >= 1e30:
+            result["host_path"] = {"error": repr(err)[:200] if err else "failed on another rank"}
+        else:
+            result["host_path"] = {"verifies_per_s": round(hs * world / hel, 1), "requests_per_gpu": hs,
+                                   "seconds": round(hel, 4), "ok": bool(np.array_equal(hv, want_local[:hs])),
+                                   "note": "pv_verify_batch from host buffers on every rank at once, PCIe "
+                                           "included, max over ranks"}
     if comb and not args.no_straus and world == 1:
         # the same batch forced through the per-request Straus path (what a batch of all-distinct
         # keys gets): reported beside the headline, never as `value`
