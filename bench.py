@@ -500,7 +500,11 @@ def main():
     elif world == 1 and not args.no_ingress:
         blob0, off, pks, *wire = nym_workload.generate_wire(rank * n, n)
     else:
-        blob0, off, pks = nym_workload.generate(rank * n, n)
+        # configs[4] shards are 8-32M requests per rank: more signing workers per rank where the node
+        # has the cores (16 is the per-GPU CPU share of a 1-GPU box; never above 64)
+        cores = len(os.sched_getaffinity(0))
+        workers = min(64, max(16, cores // world)) if world > 1 else None
+        blob0, off, pks = nym_workload.generate(rank * n, n, workers=workers)
     gen_s = time.perf_counter() - t0
     log("rank %d: generated %d requests (%.1f MB) in %.1f s" % (rank, n, blob0.nbytes / 1e6, gen_s))
     # the headline batch carries must-reject records: ~0.1 % of messages with one flipped byte
