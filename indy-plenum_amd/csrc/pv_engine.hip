@@ -230,6 +230,9 @@ struct Gate {
 //   comb_key [kcap]    key id of comb index j;  key_flag [kcap]  libsodium key checks passed
 //   bases    [kcap][32][4][10] uint4 [256^i](-A) and its [16], [32], [64] multiples, extended
 //   ctab     [kcap][32][129][10] uint4  T_A, cached form
+//   key_cslot [stride] / comb_cslot [kcap]  node-side key cache slot of a key id / comb index: a key
+//            in the cache is a comb key whatever its request count, its T_A is the cache's table
+//            and the key stream (chain, fill) skips it
 // A key takes the comb path when it carries >= min_req requests of the chunk (the per-key table
 // costs about as much as ~50 requests save; 1 when the comb path is forced) and fewer than kcap
 // keys came before it; the rest -- singletons such as the adversarial keys of config 3 -- take the
@@ -259,10 +262,14 @@ struct KeyWork {
     uint32_t* req_pos;
     uint32_t* skey;
     uint64_t* sverdict;
+    uint32_t* key_cslot;   // [stride] node-side key cache slot of key id (PV_EMPTY: not cached)
+    uint32_t* comb_cslot;  // [kcap] the same per comb index: its table is read from the cache
+    const uint4* kc_tab;   // the cache's tables [cap][32][129][10] (keycache.h)
     uint32_t hmask;
     uint32_t kcap;
     uint32_t seed;
     uint32_t min_req;
+    uint32_t kc_on;  // this launch consults the key cache (pv_key_cache_probe_kernel ran)
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 #ifndef PV_COMB_MIN_REQ
@@ -314,10 +321,24 @@ __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, con
     wk.flags[i] = ok ? 1u : 0u;
 }
 
+// Optional wave priority (s_setprio) for the Straus-path kernels, which in a split chunk run on
+// their own stream beside the comb kernels. A/B on config 3 (tools/ab_config3.sh,
+// profiles/r02/ab_straus_prio.txt): priority 3 shortens the wait for the Straus side (msm stage
+// 1.55 -> 1.45 ms) but slows the key stream's table fill more (0.92 -> 1.07 ms): off by default.
+#ifndef PV_STRAUS_PRIO
+#define PV_STRAUS_PRIO 0
+#endif
+__device__ __forceinline__ void pv_straus_prio() {
+#if PV_STRAUS_PRIO > 0
+    __builtin_amdgcn_s_setprio(PV_STRAUS_PRIO);
+#endif
+}
+
 // Kernel 1 (Straus path): pv_prep_slot over the Straus slots.
 __global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(const uint8_t* __restrict__ sm,
                                                                const uint64_t* __restrict__ off, uint64_t n,
                                                                const uint8_t* __restrict__ pk, Work wk, Gate gate) {
+    pv_straus_prio();
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t sb = gate.stile(t, ntiles);
@@ -329,6 +350,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(co
 
 // Kernel 1b: expand -A (extended, in slot 1) into the cached table [j](-A), j = 0..8.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk, Gate gate) {
+    pv_straus_prio();
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t sb = gate.stile(t, ntiles);
@@ -358,6 +380,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
     // nothing for this block (or no Straus slot at all): leave before the LDS fill
     if (blockIdx.x >= ntiles || nc >= n || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;
+    pv_straus_prio();
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
     for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
         reinterpret_cast<uint4*>(sbt)[t] = reinterpret_cast<const uint4*>(btab_g)[t];
@@ -449,6 +472,17 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, Key
     kw.key_count[id] = kw.slot_cnt[s];
 }
 
+// Dedup 2b (only when the node-side key cache holds keys): every distinct key id looks its key up
+// in the cache (keycache.h); key_cslot[id] = its cache slot or PV_EMPTY.
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_cache_probe_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
+                                                                       PvKeyCacheView kc) {
+    const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (id >= kw.nkeys[PV_SPLIT_KEYS]) return;
+    uint32_t A[8];
+    pv_load_pk(A, pk, kw.key_owner[id]);
+    kw.key_cslot[id] = pv_kc_lookup(kc, A);
+}
+
 // Exclusive prefix sum of one value per thread over a 1024-thread workgroup; *total = the sum.
 __device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
     const uint32_t t = threadIdx.x;
@@ -469,20 +503,24 @@ __device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
 // Comb keys (>= min_req requests, the first kcap of them in id order) take slots [0, CS) in id
 // order, every other key's requests the slots [CS, n). Threads own contiguous id ranges; three
 // passes over key_count: comb index, slot totals, cursors.
-__global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
+__global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uint32_t* __restrict__ kc_flags) {
     __shared__ uint32_t part[1024];
     const uint32_t nk = kw.nkeys[PV_SPLIT_KEYS];
     const uint32_t t = threadIdx.x;
     const uint32_t per = (nk + 1023) / 1024;
     const uint32_t lo = min(t * per, nk), hi = min(lo + per, nk);
+    // a key in the node-side cache costs no table build: it is a comb candidate at any count
+    auto is_cand = [&](uint32_t id, uint32_t c) {
+        return c >= kw.min_req || (kw.kc_on && kw.key_cslot[id] != PV_EMPTY);
+    };
     uint32_t cand = 0;
-    for (uint32_t id = lo; id < hi; id++) cand += kw.key_count[id] >= kw.min_req ? 1u : 0u;
+    for (uint32_t id = lo; id < hi; id++) cand += is_cand(id, kw.key_count[id]) ? 1u : 0u;
     uint32_t ncand;
     const uint32_t jbase = pv_block_scan(cand, part, &ncand);
     uint32_t cs = 0, ss = 0;
     for (uint32_t id = lo, j = jbase; id < hi; id++) {
         const uint32_t c = kw.key_count[id];
-        if (c >= kw.min_req && j++ < kw.kcap) cs += c;
+        if (is_cand(id, c) && j++ < kw.kcap) cs += c;
         else ss += c;
     }
     uint32_t ctotal, stotal;
@@ -490,9 +528,14 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
     uint32_t sc = ctotal + pv_block_scan(ss, part, &stotal);
     for (uint32_t id = lo, j = jbase; id < hi; id++) {
         const uint32_t c = kw.key_count[id];
-        if (c >= kw.min_req && j < kw.kcap) {
+        const bool cand_id = is_cand(id, c);
+        if (cand_id && j < kw.kcap) {
+            const uint32_t cslot = kw.kc_on ? kw.key_cslot[id] : PV_EMPTY;
             kw.key_cid[id] = j;
             kw.comb_key[j] = id;
+            kw.comb_cslot[j] = cslot;
+            // a cached key's libsodium checks ran when its table was built (the chain skips it)
+            if (cslot != PV_EMPTY) kw.key_flag[j] = kc_flags[cslot];
             kw.key_cursor[id] = cc;
             cc += c;
         } else {
@@ -500,7 +543,7 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw) {
             kw.key_cursor[id] = sc;
             sc += c;
         }
-        if (c >= kw.min_req) j++;
+        if (cand_id) j++;
     }
     if (t == 0) {
         kw.nkeys[PV_SPLIT_COMB_KEYS] = min(ncand, kw.kcap);
@@ -692,7 +735,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_kernel(const uint8_t
     if (!gate.keyed()) return;
     __builtin_amdgcn_s_setprio(3);
     const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;  // comb index
-    if (id >= kw.nkeys[PV_SPLIT_COMB_KEYS]) return;
+    if (id >= kw.nkeys[PV_SPLIT_COMB_KEYS] || kw.comb_cslot[id] != PV_EMPTY) return;
     uint32_t A[8];
     pv_load_pk(A, pk, kw.key_owner[kw.comb_key[id]]);
     ge_p3 negA;
@@ -777,7 +820,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const ui
     asm volatile("" : "+v"(rl));  // opaque: keep the per-role selects branch-free
     const QuadRole role{rl == 0 ? ~0u : 0u, rl == 1 ? ~0u : 0u, rl == 2 ? ~0u : 0u};
     // whole quads exit together (nk is uniform), so the DPP partners of a live lane are live
-    if (id >= nk) return;
+    if (id >= nk || kw.comb_cslot[id] != PV_EMPTY) return;  // uniform per quad
     uint32_t A[8];
     pv_load_pk(A, pk, kw.key_owner[kw.comb_key[id]]);
     ge_p3 cur;
@@ -849,7 +892,7 @@ __global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __re
     const LpLane c = LpLane::make();
     const LpConsts K = LpConsts::make(c);
     for (uint32_t id = blockIdx.x; id < nk; id += gridDim.x)
-        pv_key_chain_lp(pk, kw, id, c, K);
+        if (kw.comb_cslot[id] == PV_EMPTY) pv_key_chain_lp(pk, kw, id, c, K);  // cached: table ready
 #endif
 }
 
@@ -859,6 +902,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kerne
     const uint32_t items = kw.nkeys[PV_SPLIT_COMB_KEYS] * PV_COMB_POS * PV_COMB_BLOCKS;
     for (uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x; it < items; it += gridDim.x * PV_BLOCK) {
         const uint32_t id = it / (PV_COMB_POS * PV_COMB_BLOCKS);
+        if (kw.comb_cslot[id] != PV_EMPTY) continue;  // the key's table is in the node-side cache
         const int pos = (it / PV_COMB_BLOCKS) % PV_COMB_POS;
         const int b = it % PV_COMB_BLOCKS;
         const DevBasePts pts{DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10}, pos};
@@ -975,6 +1019,9 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
     const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
     const uint32_t id = kw.skey[i];  // comb index
+    const uint32_t cslot = kw.comb_cslot[id];
+    const uint4* ktab = cslot != PV_EMPTY ? kw.kc_tab + (uint64_t)cslot * PV_COMB_POS * PV_COMB_ENT * 10
+                                          : kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10;
     const uint32_t S = (uint32_t)wk.stride;
     const Soa qs(wk.q, 40, wk.stride);
     ge_p3 acc;
@@ -990,12 +1037,9 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
 #if PV_COMB_PIPELINE
     __shared__ uint4 stg[PV_BLOCK / 64][10][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    pv_comb_a_xyz_staged(X, Y, Z, acc,
-                         DevCombStage{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10, &stg[wv][0][0],
-                                      threadIdx.x & 63u},
-                         dig);
+    pv_comb_a_xyz_staged(X, Y, Z, acc, DevCombStage{ktab, &stg[wv][0][0], threadIdx.x & 63u}, dig);
 #else
-    const DevCombRows arows{kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10};
+    const DevCombRows arows{const_cast<uint4*>(ktab)};
     pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
 #endif
     if (kw.key_flag[id] == 0) wk.flags[i] = 0;
@@ -1269,12 +1313,20 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         // path (~3 vs ~13 ns), so AUTO gives a table to keys with >= PV_COMB_MIN_REQ requests in
         // the chunk and verifies every other request on the Straus path in the same launch. The
         // split is computed on the device by the dedup/sort kernels (Gate); nothing synchronises.
-        // Chunks below PV_KEYED_MIN requests skip dedup (~0.3 ms of fixed work) and go Straus.
-        const bool keyed = g_ctx.path == PV_PATH_COMB || (g_ctx.path == PV_PATH_AUTO && m >= PV_KEYED_MIN);
+        // Chunks below PV_KEYED_MIN requests skip dedup (~0.3 ms of fixed work) and go Straus --
+        // unless the node-side key cache holds keys: a cached key's comb table is already built, so
+        // any chunk above the latency path's range goes keyed and its cached keys' requests take
+        // the comb path at any count (48 table additions instead of the Straus loop).
+        const PvKeyCacheView kcv = kc_view();
+        const bool kc_active = kcv.hmask != 0;
+        const bool keyed = g_ctx.path == PV_PATH_COMB ||
+                           (g_ctx.path == PV_PATH_AUTO && (m >= PV_KEYED_MIN || (kc_active && m > PV_LATENCY_MAX)));
         Gate gate{nullptr, nullptr};
         g_ctx.last_keyed = keyed;
         KeyWork kw = g_ctx.kw;
         kw.min_req = g_ctx.path == PV_PATH_COMB ? 1u : (uint32_t)PV_COMB_MIN_REQ;
+        kw.kc_on = kc_active ? 1u : 0u;
+        kw.kc_tab = g_ctx.kc.d_tab;
         const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
         if (keyed) {
             PV_HIP(hipMemsetAsync(kw.slot, 0xFF, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
@@ -1284,9 +1336,14 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            if (kc_active) {
+                hipLaunchKernelGGL(pv_key_cache_probe_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0,
+                                   kw, kcv);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            }
             gate = Gate{kw.nkeys, kw.slot_req};
             // key-sorted slot order: comb keys' requests first, then the Straus requests
-            hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(1024), 0, stream, kw);
+            hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(1024), 0, stream, kw, (const uint32_t*)g_ctx.kc.d_flags);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_scatter_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -1319,8 +1376,13 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             // would delay the whole comb path. Their blocks are dispatched from the END of the slot
             // range (where the Straus slots are), and blocks of comb slots exit at once.
             hipStream_t ss = g_ctx.sstream;
-            const unsigned sgrid = std::min<unsigned>(grid, 2u * (unsigned)std::max(1, g_ctx.cus));
+#ifndef PV_SIDE_GRID_PER_CU
+#define PV_SIDE_GRID_PER_CU 2
+#endif
+            const unsigned sgrid = std::min<unsigned>(
+                grid, std::max(1u, (unsigned)(PV_SIDE_GRID_PER_CU * std::max(1, g_ctx.cus))));
             PV_HIP(hipStreamWaitEvent(ss, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
+#ifndef PV_AB_NO_SIDE  // measurement-only switch: drops the Straus side (wrong verdicts if it has work)
             hipLaunchKernelGGL(pv_prep_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -1329,6 +1391,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             hipLaunchKernelGGL(pv_msm_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                g_ctx.d_btab, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#endif
             PV_HIP(hipEventRecord(g_ctx.ev_straus_done, ss), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, kw, gate);
@@ -1442,6 +1505,9 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.req_pos, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.skey, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.sverdict, S / 64 * 8), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_cslot, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.comb_cslot, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMemset(kw.comb_cslot, 0xFF, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         std::vector<uint32_t> bc((size_t)PV_BCOMB_POS * PV_BCOMB_ENT * PV_BCOMB_STRIDE);
         {
             ge_p3 base[PV_BCOMB_POS];
@@ -1477,7 +1543,8 @@ void pv_shutdown(void) {
                     (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
                     (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb, (void*)g_ctx.kw.key_count,
                     (void*)g_ctx.kw.key_cursor, (void*)g_ctx.kw.slot_req, (void*)g_ctx.kw.req_pos,
-                    (void*)g_ctx.kw.skey, (void*)g_ctx.kw.sverdict})
+                    (void*)g_ctx.kw.skey, (void*)g_ctx.kw.sverdict, (void*)g_ctx.kw.key_cslot,
+                    (void*)g_ctx.kw.comb_cslot})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : g_ctx.ev) (void)hipEventDestroy(e);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
@@ -1792,6 +1859,7 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
         PV_HIP(hipMemcpyAsync(k.d_put_pk, bpk.data(), bpk.size(), hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemcpyAsync(k.d_put_slot, bslot.data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, 12, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        PV_HIP(hipMemsetAsync(kw.comb_cslot, 0xFF, (uint64_t)m * 4, s), PV_ERR_LAUNCH);  // build every table
         const Gate gate{kw.nkeys, kw.slot_req};
         hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(m, PV_LP_CHAIN_BLOCKS)), dim3(64), 0, s,
                            k.d_put_pk, kw, gate);

@@ -10,7 +10,7 @@ timeout -k 10 300 python3 tools/nym_workload.py --out $DS > /dev/null || exit $?
 for r in $(seq 1 $ROUNDS); do
   for v in "$@"; do
     out=$(PLENUM_AMD_LIB=microbench/variants/$v.so timeout -k 10 200 python3 bench.py --dataset $DS --no-cpu-baseline \
-          --no-host-path --no-ingress --no-config3 --no-multisig --steps 30 --warmup 3 2>/dev/null | tail -1) || exit $?
+          --no-host-path --no-ingress --no-config3 --no-multisig ${AB_EXTRA:-} --steps 30 --warmup 3 2>/dev/null | tail -1) || exit $?
     echo "$out" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); p=d['pipeline']; s=d.get('straus_path',{}); print('$v', d['ms_per_step'], {k: p[k] for k in ('keys_ms','prep_ms','table_ms','msm_ms','encode_ms')}, d['verdicts_ok'], 'straus', s.get('ms_per_step'), s.get('stages_ms'), s.get('verdicts_ok'))"
   done
 done

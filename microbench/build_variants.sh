@@ -1,14 +1,21 @@
 #!/bin/bash
-# Build engine variants (compile-time switches) next to each other for A/B timing on the GPU:
+# Build engine variants (compile-time switches of csrc/pv_engine.hip) next to each other for A/B
+# timing on the GPU:
 #   microbench/build_variants.sh NAME "-DFLAG=.. ..." [NAME "FLAGS" ...]  -> microbench/variants/NAME.so
-# Load one with PLENUM_AMD_LIB=microbench/variants/NAME.so (tests/perf_quick.py, bench.py).
+# Only the engine is recompiled with the flags; the other objects come from the in-tree build
+# (make -C indy-plenum_amd first). Load one with PLENUM_AMD_LIB=microbench/variants/NAME.so
+# (tests/perf_quick.py, bench.py).
 cd "$(dirname "$0")/../indy-plenum_amd" || exit 1
-SRC="csrc/pv_engine.hip csrc/pv_latency.hip csrc/pv_ingress.hip csrc/host_prep.cpp csrc/signing_json.cpp"
+mkdir -p ../microbench/variants
+OTHERS="build/pv_latency.hip.o build/pv_ingress.hip.o build/host_prep.cpp.o build/signing_json.cpp.o"
+for o in $OTHERS; do [ -f "$o" ] || { echo "missing $o: run make -C indy-plenum_amd" >&2; exit 1; }; done
 pids=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared $flags -o ../microbench/variants/$name.so $SRC \
-    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib > ../microbench/variants/$name.build.txt 2>&1 &
+  V=../microbench/variants/$name
+  ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -Wall $flags -c -o $V.engine.o csrc/pv_engine.hip &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o $V.so $V.engine.o $OTHERS \
+      -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib && rm -f $V.engine.o ) > $V.build.txt 2>&1 &
   pids+=($!)
 done
 rc=0

@@ -1,7 +1,9 @@
 """GPU: the node-side key cache (pv_key_cache_*). A cached key is verified on the latency path with
 32 comb-table additions instead of 252 doublings; verdicts must stay exactly libsodium's, including
 keys that fail libsodium's key checks (their tables are built with the failing flag), mixed-order
-keys with honest signatures, eviction and clearing. The throughput paths never read the cache."""
+keys with honest signatures, eviction and clearing. Above the latency path's range the keyed comb
+path reads a cached key's table instead of building it (any request count), so medium batches of
+cached signers take 48 table additions per request instead of the Straus loop."""
 import numpy as np
 import pytest
 
@@ -87,3 +89,64 @@ def test_eviction_and_clear(nat, sodium, oracle):
     assert kc.stats() == (10, 16)
     assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
     nat.set_path(nat.PV_PATH_AUTO)
+
+
+def _keyed_batch(sodium, oracle, seed):
+    """~12k requests: 20 cached signers with ~400 requests, 10 cached with 5, 10 uncached with ~300
+    (tables built in the launch), 20 uncached with 10 (Straus side), cached keys that fail
+    libsodium's key checks, and ~4 % adversarial records of every class."""
+    g = VectorGen(sodium, oracle, seed=seed)
+    keys = [g.key(i) for i in range(60)]
+    bad = [g.make(c)[1] for c in ("A_blacklist", "A_noncanonical", "A_offcurve", "mixed_order_A", "mixed_order_A")]
+    rng = np.random.default_rng(seed)
+    plan = [(k, 400) for k in range(20)] + [(k, 5) for k in range(20, 30)] + \
+           [(k, 300) for k in range(30, 40)] + [(k, 10) for k in range(40, 60)]
+    cases = []
+    for k, cnt in plan:
+        pk, sk = keys[k]
+        for _ in range(cnt):
+            m = bytes(rng.integers(0, 256, int(rng.integers(0, 320)), dtype=np.uint8))
+            sm = sodium.sign_detached(m, sk) + m
+            if rng.random() < 0.03:
+                sm = bytearray(sm)
+                sm[int(rng.integers(0, len(sm)))] ^= 1 << int(rng.integers(0, 8))
+                sm = bytes(sm)
+            cases.append((sm, pk))
+    for j in range(150):  # honest signatures under the bad keys' bytes
+        cases.append((cases[j][0], bad[j % len(bad)]))
+    for _ in range(480):
+        cases.append(g.make(VectorGen.CLASSES[1 + int(rng.integers(0, len(VectorGen.CLASSES) - 1))]))
+    order = rng.permutation(len(cases))
+    return [cases[i] for i in order], [k for k, _ in keys], bad
+
+
+def test_cached_keys_on_keyed_path(nat, sodium, oracle):
+    cases, keys, bad = _keyed_batch(sodium, oracle, seed=53)
+    blob, off, pks = pack(cases)
+    want = _want(sodium, cases)
+    kc = nat.KeyCache
+    kc.configure(64)
+    kc.put(keys[:30] + bad)
+    nat.set_path(nat.PV_PATH_AUTO)
+    got = nat.verify_sm_batch(blob, off, pks)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    path, nkeys = nat.last_path()
+    assert path == nat.PV_PATH_COMB  # keyed although the batch is below the dedup threshold
+    keys_all, comb_keys, comb_req = nat.last_split()
+    # every cached key (30 signers + the bad keys) plus the 10 uncached signers with ~300 requests
+    assert comb_keys >= 30 + 10, (keys_all, comb_keys, comb_req)
+    for name in ("comb", "straus", "latency"):
+        nat.set_path(getattr(nat, "PV_PATH_" + name.upper()))
+        got = nat.verify_sm_batch(blob, off, pks)
+        assert np.array_equal(got, want), (name, np.nonzero(got != want)[0][:10])
+    nat.set_path(nat.PV_PATH_AUTO)
+    # eviction between launches: the evicted keys' requests fall back to tables built in the launch
+    # or the Straus side, the newly cached ones read the cache
+    kc.put(keys[30:60])  # 60 > 64 - 35 free slots: the least recently put are evicted
+    assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+    kc.enable(False)
+    assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+    assert nat.last_path()[0] == nat.PV_PATH_STRAUS  # below the dedup threshold without the cache
+    kc.enable(True)
+    kc.clear()
+    assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
