@@ -298,6 +298,157 @@ PV_HD void pv_comb_xyz(fe& X, fe& Y, fe& Z, const ARows& arows, const BRows& bro
 #endif
 }
 
+// ---------------------------------------------------------------- wide fixed-base comb
+// [S]B from a radix-2^W comb held in HBM (288 GB per MI355X: the table is sized for it, not for the
+// 256 MB Infinity Cache):  T_B2[j][d] = [d 2^(W j)] B,  j = 0..P-1,  d = 0..2^(W-1) (the top row
+// 0..2^TOP), affine niels form, 128 B per entry. W = 24: P = 11 additions per request instead of
+// the radix-65536 comb's 16, a 10.7 GB table built on the device at pv_init
+// (pv_bc2_build_kernel). Digits: sc_recode_w<W, P>. W = 16 reproduces the radix-65536 comb's
+// digits and table (host tests run this code over it).
+#ifndef PV_BCOMB_W
+#define PV_BCOMB_W 24
+#endif
+static constexpr int PV_BC2_W = PV_BCOMB_W;
+static constexpr int PV_BC2_POS = (253 + PV_BC2_W - 1) / PV_BC2_W;
+static constexpr int PV_BC2_TOPBITS = 253 - PV_BC2_W * (PV_BC2_POS - 1);
+static constexpr uint32_t PV_BC2_ENT = (1u << (PV_BC2_W - 1)) + 1u;        // rows 0 .. P-2
+static constexpr uint32_t PV_BC2_TOP_ENT = (1u << PV_BC2_TOPBITS) + 1u;     // row P-1
+static_assert(PV_BC2_TOP_ENT <= PV_BC2_ENT, "top row larger than a full row");
+
+// acc = [S]B = sum_j T[j][e_j] for P positions, digit(j) = e_j (signed). The top position's entry
+// is converted to an extended point instead of being added to the identity (X = y+x - (y-x),
+// Y = y+x + y-x, Z = 2, T = X Y / 2: two products instead of an addition's seven); then P - 1 niels
+// additions, each staging the next position's entry while it multiplies (st.stage / st.staged as in
+// pv_comb_b_acc_staged).
+template <int P, class BStage, class Digit>
+PV_HD void pv_comb_b_acc_w(ge_p3& acc, const BStage& st, const Digit& digit) {
+    int f = digit(P - 1);
+    st.stage(P - 1, f < 0 ? -f : f);
+    {
+        uint32_t w[20];
+        st.staged(0, w);
+        fe ypx, ymx, h;
+        pv_sel_pm(ypx, ymx, w, f < 0);
+        f = digit(P - 2);
+        st.stage(P - 2, f < 0 ? -f : f);
+        fe_sub(acc.X, ypx, ymx);
+        fe_carry(acc.X, acc.X);
+        fe_add(acc.Y, ypx, ymx);
+        fe_carry(acc.Y, acc.Y);
+        fe_0(acc.Z);
+        acc.Z.v[0] = 2;
+        fe_const(h, PV_INV2);
+        fe_mul(acc.T, acc.X, acc.Y);
+        fe_mul(acc.T, acc.T, h);
+    }
+    ge_p1p1 t;
+    for (int j = P - 2; j >= 0; j--) {
+        const bool neg = f < 0;
+        uint32_t w[20];
+        st.staged(0, w);
+        fe ypx, ymx, xy2d, tt, a, b, c, d;
+        pv_sel_pm(ypx, ymx, w, neg);
+        const int fn = j > 0 ? digit(j - 1) : 0;  // lands during the two products
+        fe_sub(tt, acc.Y, acc.X);
+        fe_mul(a, tt, ymx);
+        fe_add(tt, acc.Y, acc.X);
+        fe_mul(b, tt, ypx);
+        st.staged(1, w);
+#pragma unroll
+        for (int i = 0; i < 10; i++) xy2d.v[i] = w[i];
+        if (j > 0) {
+            f = fn;
+            st.stage(j - 1, f < 0 ? -f : f);
+        }
+        fe_cneg(xy2d, xy2d, neg);
+        fe_mul(c, acc.T, xy2d);
+        fe_add(d, acc.Z, acc.Z);  // 2 Z, not carried (see ge_add_niels)
+        fe_sub(t.X, b, a);
+        fe_add(t.Y, b, a);
+        fe_add(t.Z, d, c);
+        fe_sub(t.T, d, c);
+        ge_niels_p1p1_to_p3(acc, t);
+    }
+}
+
+// Wide fixed-base comb build, one run of cnt consecutive entries d0 .. d0 + cnt - 1 of the row of
+// base point P (pv_bc2_build_kernel: one run per thread): the start [d0] P by double-and-add, then
+// P-steps, each projective point parked in its own entry (row.e(d): 32 words) with the running
+// product of the Z's in scr; ONE inversion per run (Montgomery's trick) then gives every entry's
+// affine niels form (y+x, y-x, 2dxy) in canonical limbs -- the same entries as
+// pv_bcomb_build_position for W = 16 (host test).
+template <class Row, class Scr>
+PV_HD void pv_bc2_build_run(const Row& row, const Scr& scr, const ge_p3& P, uint32_t d0, uint32_t cnt) {
+    ge_cached cP;
+    ge_p3_to_cached(cP, P);
+    ge_p3 cur;
+    ge_p3_identity(cur);
+    ge_p1p1 t;
+    for (int b = 31; b >= 0; b--) {
+        if (d0 >> (b + 1)) {
+            ge_p2_dbl(t, cur.X, cur.Y, cur.Z);
+            ge_p1p1_to_p3(cur, t);
+        }
+        if ((d0 >> b) & 1u) {
+            ge_add_cached(t, cur, cP);
+            ge_p1p1_to_p3(cur, t);
+        }
+    }
+    fe prod;
+    fe_1(prod);
+    for (uint32_t k = 0; k < cnt; k++) {
+        uint32_t* e = row.e(d0 + k);
+        fe_mul(prod, prod, cur.Z);
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            e[q] = cur.X.v[q];
+            e[10 + q] = cur.Y.v[q];
+            e[20 + q] = cur.Z.v[q];
+        }
+        scr.store(d0 + k, prod);
+        ge_add_cached(t, cur, cP);
+        ge_p1p1_to_p3(cur, t);
+    }
+    fe inv, d2;
+    fe_invert(inv, prod);
+    fe_const(d2, PV_D2);
+    for (int k = (int)cnt - 1; k >= 0; k--) {
+        uint32_t* e = row.e(d0 + (uint32_t)k);
+        fe X, Y, Z, zi, x, y, tt, ypx, ymx, xy2d;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            X.v[q] = e[q];
+            Y.v[q] = e[10 + q];
+            Z.v[q] = e[20 + q];
+        }
+        if (k > 0) {
+            fe prev;
+            scr.load(d0 + (uint32_t)k - 1, prev);
+            fe_mul(zi, inv, prev);
+        } else {
+            fe_copy(zi, inv);
+        }
+        fe_mul(inv, inv, Z);
+        fe_mul(x, X, zi);
+        fe_mul(y, Y, zi);
+        fe_add(tt, y, x);
+        fe_canonical(ypx, tt);
+        fe_sub(tt, y, x);
+        fe_canonical(ymx, tt);
+        fe_mul(tt, x, y);
+        fe_mul(tt, tt, d2);
+        fe_canonical(xy2d, tt);
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            e[q] = ypx.v[q];
+            e[10 + q] = ymx.v[q];
+            e[20 + q] = xy2d.v[q];
+        }
+        e[30] = 0;
+        e[31] = 0;
+    }
+}
+
 // ---------------------------------------------------------------- fixed-base comb (host, init)
 // T_B[j][d] = [d 65536^j] B in affine niels form (y+x, y-x, 2dxy), canonical limbs, PV_BCOMB_STRIDE
 // words per entry. Built on the host: one thread per position (16), each with one batched

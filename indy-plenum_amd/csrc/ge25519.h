@@ -25,6 +25,9 @@ static constexpr uint32_t PV_D[10] = {0x35978a3u, 0x0d37284u, 0x3156ebdu, 0x06a0
                                       0x179e898u, 0x3a03cbbu, 0x1ce7198u, 0x2e2b6ffu, 0x1480db3u};
 static constexpr uint32_t PV_D2[10] = {0x2b2f159u, 0x1a6e509u, 0x22add7au, 0x0d4141du, 0x0038052u,
                                        0x0f3d130u, 0x3407977u, 0x19ce331u, 0x1c56dffu, 0x0901b67u};
+// 1/2 = (p + 1) / 2
+static constexpr uint32_t PV_INV2[10] = {0x3fffff7u, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu,
+                                         0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu, 0x0ffffffu};
 static constexpr uint32_t PV_SQRTM1[10] = {0x20ea0b0u, 0x186c9d2u, 0x08f189du, 0x035697fu, 0x0bd0c60u,
                                            0x1fbd7a7u, 0x2804c9eu, 0x1e16569u, 0x004fc1du, 0x0ae0c92u};
 

@@ -161,13 +161,17 @@ struct LdsBTab {
 
 // Digit words of k (radix 16, rows 0..7) and S (radix 256, rows 8..15), one coalesced load each time
 // the Straus loop enters a new group of 8 windows.
+// digits rows: 0..7 k (both paths), 8.. S: 8 packed words (Straus, radix 256) or PV_BC2_POS signed
+// radix-2^W digits (comb path, wide fixed-base comb)
+static constexpr int PV_DIGIT_ROWS = 8 + (PV_BC2_POS > 8 ? PV_BC2_POS : 8);
 struct DevDigits {
     Soa d;
     uint32_t slot;
     __device__ __forceinline__ DevDigits(uint32_t* base, uint32_t stride, uint32_t slot_)
-        : d(base, 16, stride), slot(slot_) {}
+        : d(base, PV_DIGIT_ROWS, stride), slot(slot_) {}
     __device__ __forceinline__ uint32_t ek(int q) const { return d.ld(q, slot); }
     __device__ __forceinline__ uint32_t fs(int q) const { return d.ld(8 + q, slot); }
+    __device__ __forceinline__ int fb(int j) const { return (int)d.ld(8 + j, slot); }
 };
 
 // Request bytes at an arbitrary byte offset: aligned dword loads + v_alignbyte_b32 funnel shifts.
@@ -185,7 +189,8 @@ struct DevMsg {
 
 // Per-request intermediate state between the two kernels (SoA, coalesced per wave):
 //   atab  [9 entries][10 quads][n] uint4   cached [j](-A), j = 0..8
-//   digits[16][n] uint32                    radix-16 digits of k (8 words), radix-256 of S (8 words)
+//   digits[PV_DIGIT_ROWS][n] uint32          radix-16 digits of k (8 words), radix-256 of S (8 words);
+//                                           comb path: radix-256 k, radix-2^W S (PV_BC2_POS words)
 //   flags [n] uint32                        1 = every libsodium pre-check passed
 //   q     [40][n] uint32                    projective Q = (X, Y, Z) from the msm kernel (rows 0..29);
 //                                           the comb path's [S]B half parks an extended point here
@@ -312,7 +317,7 @@ __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, con
     uint32_t ek[8], fs[8];
     sc_recode16(ek, k);
     sc_recode256(fs, in.S);
-    const Soa ds(wk.digits, 16, wk.stride);
+    const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         ds.st(q, (uint32_t)i, ek[q]);
@@ -955,21 +960,46 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
     pv_hash_k(k, in, smlen, mw);
     // the key's own checks (key_flag) are written by the chain kernel on the key stream, which
     // runs concurrently with this kernel: pv_comb_a_kernel folds them into flags[slot]
-    uint32_t ek[8], fs[8];
+    uint32_t ek[8];
+    int32_t fb[PV_BC2_POS];
     sc_recode256(ek, k);
-    sc_recode65536(fs, in.S);
-    const Soa ds(wk.digits, 16, wk.stride);
+    sc_recode_w<PV_BC2_W, PV_BC2_POS>(fb, in.S);
+    const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-        ds.st(q, i, ek[q]);
-        ds.st(8 + q, i, fs[q]);
-    }
+    for (int q = 0; q < 8; q++) ds.st(q, i, ek[q]);
+#pragma unroll
+    for (int j = 0; j < PV_BC2_POS; j++) ds.st(8 + j, i, (uint32_t)fb[j]);
     wk.flags[i] = ok ? 1u : 0u;
 }
 
-// Per request on the comb path, first half: acc = [S]B from the fixed-base comb (16 additions).
-// Needs no per-key data, so it runs on the main stream while the key stream builds the tables.
-// acc (extended, 40 words) goes to q rows 0..39.
+// Wide fixed-base comb rows (comb.h PV_BC2_*): row j = entries 0..PV_BC2_ENT-1 of [d 2^(W j)] B,
+// 8 uint4 each, LDS-staged like DevBStage; 64-bit entry index (the table is ~10.7 GB at W = 24).
+struct DevB2Stage {
+    const uint4* base;
+    uint4* lds;
+    uint32_t lane;
+    __device__ __forceinline__ void stage(int j, int d) const {
+        const uint4* e = base + ((uint64_t)j * PV_BC2_ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4);
+        pv_lds_reads_done();
+        pv_glds16_row<PV_BCOMB_STRIDE / 4>(e, lds);
+    }
+    __device__ __forceinline__ void staged(int part, uint32_t w[20]) const {
+#pragma unroll
+        for (int q = 0; q < (part ? 3 : 5); q++) {
+            const uint4 v = lds[(5 * part + q) * 64 + lane];
+            const int lim = part ? 10 : 20;
+            if (4 * q < lim) w[4 * q] = v.x;
+            if (4 * q + 1 < lim) w[4 * q + 1] = v.y;
+            if (4 * q + 2 < lim) w[4 * q + 2] = v.z;
+            if (4 * q + 3 < lim) w[4 * q + 3] = v.w;
+        }
+    }
+};
+
+// Per request on the comb path, first half: acc = [S]B from the wide fixed-base comb (PV_BC2_POS
+// positions: one entry conversion + PV_BC2_POS - 1 additions). Needs no per-key data, so it runs on
+// the main stream while the key stream builds the tables. acc (extended, 40 words) goes to q rows
+// 0..39.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
                                                                  Gate gate) {
     if (!gate.keyed()) return;
@@ -977,13 +1007,10 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
     if (i >= gate.ncomb()) return;
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     ge_p3 acc;
-#if PV_COMB_PIPELINE
     __shared__ uint4 stg[PV_BLOCK / 64][PV_BCOMB_STRIDE / 4][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    pv_comb_b_acc_staged(acc, DevBStage{bcomb, &stg[wv][0][0], threadIdx.x & 63u}, dig);
-#else
-    pv_comb_b_acc(acc, DevBRows{bcomb}, dig);
-#endif
+    pv_comb_b_acc_w<PV_BC2_POS>(acc, DevB2Stage{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
+                                [&](int j) { return dig.fb(j); });
     const Soa qs(wk.q, 40, wk.stride);
 #pragma unroll
     for (int q = 0; q < 10; q++) {
@@ -992,6 +1019,45 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
         qs.st(20 + q, i, acc.Z.v[q]);
         qs.st(30 + q, i, acc.T.v[q]);
     }
+}
+
+// Wide fixed-base comb build (pv_init): each thread makes PV_BC2_RUN consecutive entries d0.. of one
+// row (base point P = [2^(W j)] B): start [d0] P by double-and-add, then P-steps, the projective
+// points parked in the entries themselves and the running product of their Z in `scratch`; one
+// inversion per run (Montgomery's trick) gives every entry's affine niels form (canonical limbs).
+static constexpr uint32_t PV_BC2_RUN = 64;
+struct PvPoint40 {
+    uint32_t w[40];  // X, Y, Z, T limbs
+};
+struct DevBc2Row {  // one row of the wide comb, 32 words per entry
+    uint32_t* r;
+    __device__ __forceinline__ uint32_t* e(uint32_t d) const { return r + (uint64_t)d * PV_BCOMB_STRIDE; }
+};
+struct DevBc2Scratch {  // running Z products, 10 words per entry
+    uint32_t* z;
+    __device__ __forceinline__ void store(uint32_t d, const fe& f) const {
+#pragma unroll
+        for (int q = 0; q < 10; q++) z[(uint64_t)d * 10 + q] = f.v[q];
+    }
+    __device__ __forceinline__ void load(uint32_t d, fe& f) const {
+#pragma unroll
+        for (int q = 0; q < 10; q++) f.v[q] = z[(uint64_t)d * 10 + q];
+    }
+};
+__global__ __launch_bounds__(PV_BLOCK) void pv_bc2_build_kernel(uint4* __restrict__ row, uint32_t ent, PvPoint40 base,
+                                                                uint32_t* __restrict__ scratch) {
+    const uint32_t d0 = (blockIdx.x * PV_BLOCK + threadIdx.x) * PV_BC2_RUN;
+    if (d0 >= ent) return;
+    ge_p3 P;
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        P.X.v[q] = base.w[q];
+        P.Y.v[q] = base.w[10 + q];
+        P.Z.v[q] = base.w[20 + q];
+        P.T.v[q] = base.w[30 + q];
+    }
+    pv_bc2_build_run(DevBc2Row{reinterpret_cast<uint32_t*>(row)}, DevBc2Scratch{scratch}, P, d0,
+                     min(PV_BC2_RUN, ent - d0));
 }
 
 // XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs (block b runs on the XCD
@@ -1143,7 +1209,8 @@ struct Ctx {
     bool last_latency = false;  // the most recent launch took the latency path
     bool verdict_zeroed = false;  // the caller's verdict words are already 0 (pv_verify_batch)
     uint32_t last_split[3] = {0, 0, 0};  // PV_SPLIT_* of it, read back by pv_last_path
-    uint4* d_bcomb = nullptr;  // fixed-base comb T_B
+    uint4* d_bcomb = nullptr;  // fixed-base comb T_B (radix 65536; latency path)
+    uint4* d_bc2 = nullptr;    // wide fixed-base comb T_B2 (radix 2^W; comb path's [S]B)
     int path = PV_PATH_AUTO;
     // host-entry staging
     uint8_t* h_stage = nullptr;  // pinned
@@ -1398,7 +1465,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             // [S]B while the key stream finishes the tables, then join
-            hipLaunchKernelGGL(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bcomb,
+            hipLaunchKernelGGL(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
                                gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
@@ -1478,7 +1545,7 @@ int pv_init(int device) {
     const uint64_t S = PV_CHUNK;
     g_ctx.work.stride = S;
     PV_HIP(hipMalloc((void**)&g_ctx.work.atab, S * 9 * 160), PV_ERR_ALLOC);
-    PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * 16 * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * PV_DIGIT_ROWS * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 40 * 4), PV_ERR_ALLOC);
     {
@@ -1520,6 +1587,46 @@ int pv_init(int device) {
         }
         PV_HIP(hipMalloc((void**)&g_ctx.d_bcomb, bc.size() * 4), PV_ERR_ALLOC);
         PV_HIP(hipMemcpy(g_ctx.d_bcomb, bc.data(), bc.size() * 4, hipMemcpyHostToDevice), PV_ERR_ALLOC);
+        // the wide fixed-base comb, built on the device row by row (one scratch row of Z products)
+        {
+            const uint64_t rows_ent = (uint64_t)(PV_BC2_POS - 1) * PV_BC2_ENT + PV_BC2_TOP_ENT;
+            PV_HIP(hipMalloc((void**)&g_ctx.d_bc2, rows_ent * PV_BCOMB_STRIDE * 4), PV_ERR_ALLOC);
+            uint32_t* scratch = nullptr;
+            PV_HIP(hipMalloc((void**)&scratch, (uint64_t)PV_BC2_ENT * 40), PV_ERR_ALLOC);
+            ge_p3 negB, P;
+            ge_frombytes_negate(negB, PV_B_ENC);
+            P = negB;
+            fe z;
+            fe_0(z);
+            fe_sub(P.X, z, negB.X);
+            fe_carry(P.X, P.X);
+            fe_sub(P.T, z, negB.T);
+            fe_carry(P.T, P.T);
+            int rc = PV_OK;
+            for (int j = 0; j < PV_BC2_POS && rc == PV_OK; j++) {
+                PvPoint40 arg;
+                for (int q = 0; q < 10; q++) {
+                    arg.w[q] = P.X.v[q];
+                    arg.w[10 + q] = P.Y.v[q];
+                    arg.w[20 + q] = P.Z.v[q];
+                    arg.w[30 + q] = P.T.v[q];
+                }
+                const uint32_t ent = j + 1 < PV_BC2_POS ? PV_BC2_ENT : PV_BC2_TOP_ENT;
+                const uint32_t threads = (ent + PV_BC2_RUN - 1) / PV_BC2_RUN;
+                hipLaunchKernelGGL(pv_bc2_build_kernel, dim3((threads + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
+                                   g_ctx.stream, g_ctx.d_bc2 + (uint64_t)j * PV_BC2_ENT * (PV_BCOMB_STRIDE / 4), ent,
+                                   arg, scratch);
+                if (hipGetLastError() != hipSuccess || hipStreamSynchronize(g_ctx.stream) != hipSuccess)
+                    rc = fail(PV_ERR_LAUNCH, "pv_init: wide fixed-base comb build failed");
+                for (int r = 0; r < PV_BC2_W; r++) {  // next row's base: 2^W P
+                    ge_p1p1 t;
+                    ge_p2_dbl(t, P.X, P.Y, P.Z);
+                    ge_p1p1_to_p3(P, t);
+                }
+            }
+            (void)hipFree(scratch);
+            if (rc != PV_OK) return rc;
+        }
     }
     g_ctx.device = device;
     return PV_OK;
@@ -1541,7 +1648,7 @@ void pv_shutdown(void) {
                     (void*)g_ctx.kw.req_rank, (void*)g_ctx.kw.nkeys,
                     (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_cid, (void*)g_ctx.kw.comb_key,
                     (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
-                    (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb, (void*)g_ctx.kw.key_count,
+                    (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb, (void*)g_ctx.d_bc2, (void*)g_ctx.kw.key_count,
                     (void*)g_ctx.kw.key_cursor, (void*)g_ctx.kw.slot_req, (void*)g_ctx.kw.req_pos,
                     (void*)g_ctx.kw.skey, (void*)g_ctx.kw.sverdict, (void*)g_ctx.kw.key_cslot,
                     (void*)g_ctx.kw.comb_cslot})

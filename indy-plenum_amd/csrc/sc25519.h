@@ -169,3 +169,32 @@ PV_HD void sc_recode65536(uint32_t out[8], const uint32_t a[8]) {
         out[w] = word;
     }
 }
+
+// Bits [lo, lo + n) of the 256-bit little-endian a (n <= 32).
+PV_HD uint32_t sc_bits(const uint32_t a[8], int lo, int n) {
+    const int i = lo >> 5, sh = lo & 31;
+    uint32_t x = a[i] >> sh;
+    if (sh && i + 1 < 8) x |= a[i + 1] << (32 - sh);
+    return n < 32 ? x & ((1u << n) - 1u) : x;
+}
+
+// Signed radix-2^W digits of a scalar for the wide fixed-base comb (comb.h, PV_BC2_*): P positions,
+// e_j in [-2^(W-1), 2^(W-1)) for j < P - 1 and the top digit e_{P-1} in [0, 2^TOP] for a < 2^253
+// (TOP = 253 - W (P - 1)). For a >= 2^253 -- S >= L, which libsodium rejects before any point
+// arithmetic (sc25519_is_canonical), so the verdict is false whatever Q is -- the top digit is clamped
+// to 2^TOP so that the table lookup stays inside the top row. For W = 16 the digits are exactly
+// sc_recode65536's (same carry rule).
+template <int W, int P>
+PV_HD void sc_recode_w(int32_t out[P], const uint32_t a[8]) {
+    constexpr int TOP = 253 - W * (P - 1);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < P - 1; j++) {
+        const uint32_t v = sc_bits(a, W * j, W) + carry;
+        carry = (v + (1u << (W - 1))) >> W;
+        out[j] = (int32_t)v - (int32_t)(carry << W);
+    }
+    uint32_t top = sc_bits(a, W * (P - 1), 256 - W * (P - 1)) + carry;
+    if (top > (1u << TOP)) top = 1u << TOP;
+    out[P - 1] = (int32_t)top;
+}

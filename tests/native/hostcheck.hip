@@ -176,6 +176,81 @@ int hc_sign_open_comb(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     return use[0] && pv_words_equal(enc[0], in.R);
 }
 
+// Wide fixed-base comb (comb.h PV_BC2_*): signed radix-2^W digits of a 32-byte scalar; returns P.
+int hc_sc_recode_w(int w, int32_t* out, const uint8_t* a) {
+    uint32_t x[8];
+    load_words(x, a);
+    switch (w) {
+        case 16: sc_recode_w<16, 16>(out, x); return 16;
+        case 20: sc_recode_w<20, 13>(out, x); return 13;
+        case 22: sc_recode_w<22, 12>(out, x); return 12;
+        case 24: sc_recode_w<24, 11>(out, x); return 11;
+        default: return 0;
+    }
+}
+
+// pv_bc2_build_run over entries [d0, d0 + cnt) of the radix-65536 row with base [65536^j] B
+// (out: cnt x 32 words), for comparison with pv_bcomb_build_position's table (W = 16).
+struct HostBc2Row {
+    uint32_t* r;
+    uint32_t d0;
+    uint32_t* e(uint32_t d) const { return r + (size_t)(d - d0) * PV_BCOMB_STRIDE; }
+};
+struct HostBc2Scratch {
+    fe* z;
+    uint32_t d0;
+    void store(uint32_t d, const fe& f) const { z[d - d0] = f; }
+    void load(uint32_t d, fe& f) const { f = z[d - d0]; }
+};
+void hc_bc2_build_run16(uint32_t* out, int j, uint32_t d0, uint32_t cnt) {
+    ge_p3 base[PV_BCOMB_POS];
+    pv_bcomb_bases(base);
+    std::vector<fe> z(cnt);
+    pv_bc2_build_run(HostBc2Row{out, d0}, HostBc2Scratch{z.data(), d0}, base[j], d0, cnt);
+}
+const uint32_t* hc_bcomb_table(void) { return host_bcomb().data(); }
+
+// crypto_sign_open through the comb path with [S]B from pv_comb_b_acc_w<16> (the wide comb's code,
+// W = 16) over the radix-65536 host table, [k](-A) from the staged per-key comb.
+int hc_sign_open_comb_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    const std::vector<uint32_t>& bcomb = host_bcomb();
+    std::vector<uint8_t> buf(smlen + 256, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    HostMsg mw{buf.data()};
+    bool ok = pv_sig_ok(in, smlen);
+    ge_p3 negA;
+    ok &= pv_key_ok_negate(negA, in.A);
+    uint32_t k[8];
+    pv_hash_k(k, in, smlen, mw);
+    std::vector<ge_p3> bases(PV_COMB_POS * PV_COMB_PTS);
+    pv_comb_chain(HostBases{bases.data()}, negA);
+    std::vector<uint32_t> ctab((size_t)PV_COMB_POS * PV_COMB_ENT * 40);
+    for (int pos = 0; pos < PV_COMB_POS; pos++)
+        for (int b = 0; b < PV_COMB_BLOCKS; b++)
+            pv_comb_fill_block(HostCombRow{ctab.data() + (size_t)pos * PV_COMB_ENT * 40},
+                               HostBasePts{bases.data() + pos * PV_COMB_PTS}, b);
+    pv_dig_regs dig;
+    sc_recode256(dig.e, k);
+    int32_t fb[16];
+    sc_recode_w<16, 16>(fb, in.S);
+    HostBRows brows{bcomb.data()};
+    ge_p3 acc;
+    pv_comb_b_acc_w<16>(acc, PvRowsStageB<HostBRows>{brows, 0, 0}, [&](int j) { return fb[j]; });
+    HostCombRows arows{ctab.data()};
+    fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
+    bool use[PV_ENC_BATCH];
+    pv_comb_a_xyz_staged(X[0], Y[0], Z[0], acc, PvRowsStageA<HostCombRows>{arows, 0, 0}, dig);
+    use[0] = ok;
+    for (int t = 1; t < PV_ENC_BATCH; t++) { X[t] = X[0]; Y[t] = Y[0]; Z[t] = Z[0]; use[t] = false; }
+    uint32_t enc[PV_ENC_BATCH][8];
+    pv_encode_batch(enc, X, Y, Z, use);
+    return use[0] && pv_words_equal(enc[0], in.R);
+}
+
 // k = SHA-512(R||A||M) mod L through pv_prepare (exposes the hashing + reduction)
 void hc_prepare_k(uint8_t* kout, const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK

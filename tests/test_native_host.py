@@ -224,3 +224,60 @@ def test_comb_path_vs_libsodium(hc, sodium, oracle):
         for _ in range(3):
             sm, pk = g.make(cls)
             assert bool(hc.hc_sign_open_comb(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
+
+
+def _recode_w(hc, w, s):
+    out = (ctypes.c_int32 * 16)()
+    p = hc.hc_sc_recode_w(w, out, s.to_bytes(32, "little"))
+    return list(out[:p])
+
+
+def test_wide_comb_recode(hc):
+    """sc_recode_w<W, P> (the wide fixed-base comb's digits of S): sum d_j 2^(W j) == S for every
+    S < 2^253, d_j in [-2^(W-1), 2^(W-1)) below the top, top in [0, 2^TOP]; S >= 2^253 (rejected by
+    the S < L check before any point arithmetic) keeps every digit inside its table row."""
+    rng = random.Random(31)
+    for w, npos in ((16, 16), (20, 13), (22, 12), (24, 11)):
+        top = 253 - w * (npos - 1)
+        vals = [0, 1, L - 1, L, 2 ** 252, 2 ** 253 - 1, (1 << (w - 1)), (1 << w) - 1] + \
+               [rng.randrange(L) for _ in range(1500)] + [rng.getrandbits(253) for _ in range(500)]
+        for s in vals:
+            d = _recode_w(hc, w, s)
+            assert len(d) == npos
+            assert sum(x << (w * j) for j, x in enumerate(d)) == s, (w, s)
+            assert all(-(1 << (w - 1)) <= x < (1 << (w - 1)) for x in d[:-1])
+            assert 0 <= d[-1] <= (1 << top)
+        for s in (2 ** 253, 2 ** 255 + 12345, 2 ** 256 - 1):
+            d = _recode_w(hc, w, s)
+            assert all(-(1 << (w - 1)) <= x < (1 << (w - 1)) for x in d[:-1]) and 0 <= d[-1] <= (1 << top)
+
+
+def test_wide_comb_build_run_matches_table(hc):
+    """pv_bc2_build_run (the device build of the wide comb, one run per thread: double-and-add start,
+    P-steps, one batched inversion) gives exactly the entries of the host-built radix-65536 table at
+    W = 16, including d = 0 (identity) and a run that ends at the row's last entry."""
+    tab = hc.hc_bcomb_table
+    tab.restype = ctypes.POINTER(ctypes.c_uint32)
+    base = tab()
+    ent, stride = 32769, 32
+    for j, d0, cnt in ((0, 0, 64), (0, 4096, 64), (5, 12345, 64), (15, 32704, 65), (9, 1000, 7)):
+        out = (ctypes.c_uint32 * (cnt * stride))()
+        hc.hc_bc2_build_run16(out, j, ctypes.c_uint32(d0), ctypes.c_uint32(cnt))
+        want = base[(j * ent + d0) * stride:(j * ent + d0 + cnt) * stride]
+        assert list(out) == list(want), (j, d0)
+
+
+def test_wide_comb_path_vs_libsodium(hc, sodium, oracle):
+    """[S]B through pv_comb_b_acc_w (entry conversion at the top position + niels additions, the
+    device comb_b code) over the radix-65536 table, then the per-key comb: every golden verdict and
+    every adversarial class against libsodium."""
+    from vectors import VectorGen
+    with open(os.path.join(HERE, "golden", "verdicts.json")) as f:
+        for c in json.load(f):
+            sm, pk = bytes.fromhex(c["sm"]), bytes.fromhex(c["pk"])
+            assert bool(hc.hc_sign_open_comb_wide16(sm, ctypes.c_uint64(len(sm)), pk)) == c["ok"], c["cls"]
+    g = VectorGen(sodium, oracle, seed=23)
+    for cls in VectorGen.CLASSES:
+        for _ in range(3):
+            sm, pk = g.make(cls)
+            assert bool(hc.hc_sign_open_comb_wide16(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
