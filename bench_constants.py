@@ -39,18 +39,21 @@ MAC_TABLE = _mac(_S_TABLE, _M_TABLE)
 MAC_LOOP = _mac(_S_LOOP, _M_LOOP)
 MAC_ENCODE = _mac(_S_ENC, _M_ENC)
 MAC_PER_VERIFY = MAC_DECOMPRESS + MAC_TABLE + MAC_LOOP + MAC_ENCODE
-# the work this build's dominant kernel (pv_msm_kernel: the Straus loop to projective Q) performs;
-# the encoding runs in pv_encode_kernel
-MAC_MSM_KERNEL = MAC_LOOP
+# The Straus path's dominant kernel (pv_msm_kernel) runs the loop over k only: [S]B comes from the
+# wide fixed-base comb in pv_straus_b_kernel (PV_STRAUS_WIDE_B) and is added once at the end. Its
+# algorithmic work is libsodium's loop without the B-scalar half of the sliding-window additions:
+# 253 doublings + 42.7 additions; the encoding runs in pv_encode_kernel.
+MAC_MSM_KERNEL = _mac(_S_LOOP, 253 * 3 + _ADDS / 2 * 8)
 
 # The keyed comb path (indy-plenum_amd/csrc/comb.h) performs a DIFFERENT algorithm for the same
 # verdict: per request 32 cached-form additions of radix-256 T_A entries (4 M + 4 M to extended) and
-# 16 affine-niels additions of radix-65536 T_B entries (3 M + 4 M), the last one to projective
-# (3 M): no doublings. Its kernel's roofline uses its own algorithmic work, counted the same way:
-MAC_COMB_MSM = MAC_PER_MUL * (32 * 8 + 16 * 7 - 1)
-# it runs as two kernels: pv_comb_b_kernel ([S]B, 16 niels additions) overlapped with the per-key
-# table build, then pv_comb_a_kernel (the 32 T_A additions, the MSM stage and the roofline kernel)
-MAC_COMB_B_KERNEL = MAC_PER_MUL * 16 * 7
+# [S]B from the radix-2^24 wide fixed-base comb (11 positions: the top entry converted to extended,
+# 2 M, then 10 affine-niels additions, 3 M + 4 M), the last T_A addition to projective (3 M): no
+# doublings. Its kernel's roofline uses its own algorithmic work, counted the same way:
+MAC_COMB_MSM = MAC_PER_MUL * (32 * 8 + 10 * 7 + 2 - 1)
+# it runs as two kernels: pv_comb_b_kernel ([S]B) overlapped with the per-key table build, then
+# pv_comb_a_kernel (the 32 T_A additions, the MSM stage and the roofline kernel)
+MAC_COMB_B_KERNEL = MAC_PER_MUL * (10 * 7 + 2)
 MAC_COMB_MSM_KERNEL = MAC_PER_MUL * (32 * 8 - 1)
 # per distinct key (amortised over the requests that share it): decompression + 31 x 8 doublings
 # (4 S + 3 M, the last of each 8 to extended: +1 M) + 32 x 129 table entries (8 M + 1 M each)

@@ -281,6 +281,12 @@ static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 #define PV_COMB_MIN_REQ 48
 #endif
 
+// Straus path: [S]B from the wide fixed-base comb (pv_straus_b_kernel) and a Straus loop over k only
+// (pv_straus_a_xyz), instead of 32 B additions interleaved in the loop (LDS table of [j]B).
+#ifndef PV_STRAUS_WIDE_B
+#define PV_STRAUS_WIDE_B 1
+#endif
+
 // Straus path, per slot i (request r): checks, decompression of A, k = SHA-512(R||A||M) mod L,
 // recoding; -A for the table kernel.
 __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, const uint64_t* __restrict__ off,
@@ -314,15 +320,22 @@ __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, con
     }
     const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
     at.store(1, w);
-    uint32_t ek[8], fs[8];
+    uint32_t ek[8];
     sc_recode16(ek, k);
-    sc_recode256(fs, in.S);
     const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-        ds.st(q, (uint32_t)i, ek[q]);
-        ds.st(8 + q, (uint32_t)i, fs[q]);
-    }
+    for (int q = 0; q < 8; q++) ds.st(q, (uint32_t)i, ek[q]);
+#if PV_STRAUS_WIDE_B
+    int32_t fb[PV_BC2_POS];  // [S]B from the wide fixed-base comb (pv_straus_b_kernel)
+    sc_recode_w<PV_BC2_W, PV_BC2_POS>(fb, in.S);
+#pragma unroll
+    for (int j = 0; j < PV_BC2_POS; j++) ds.st(8 + j, (uint32_t)i, (uint32_t)fb[j]);
+#else
+    uint32_t fs[8];
+    sc_recode256(fs, in.S);
+#pragma unroll
+    for (int q = 0; q < 8; q++) ds.st(8 + q, (uint32_t)i, fs[q]);
+#endif
     wk.flags[i] = ok ? 1u : 0u;
 }
 
@@ -386,11 +399,13 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
     // nothing for this block (or no Straus slot at all): leave before the LDS fill
     if (blockIdx.x >= ntiles || nc >= n || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;
     pv_straus_prio();
+#if !PV_STRAUS_WIDE_B
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
     for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
         reinterpret_cast<uint4*>(sbt)[t] = reinterpret_cast<const uint4*>(btab_g)[t];
     __syncthreads();
     const LdsBTab bt{sbt};
+#endif
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t sb = gate.stile(t, ntiles);
         if ((sb + 1) * PV_BLOCK <= nc) break;
@@ -399,10 +414,22 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
         const uint32_t i = active ? i0 : (uint32_t)n - 1;  // n - 1 >= nc here: a Straus slot
         const DevATab at{wk.atab, (uint32_t)wk.stride, i};
         const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
+        const Soa qs(wk.q, 40, wk.stride);
         fe X, Y, Z;
+#if PV_STRAUS_WIDE_B
+        pv_straus_a_xyz(X, Y, Z, at, dig, [&](ge_p3& accB) {  // [S]B, written by pv_straus_b_kernel
+#pragma unroll
+            for (int q = 0; q < 10; q++) {
+                accB.X.v[q] = qs.ld(q, i);
+                accB.Y.v[q] = qs.ld(10 + q, i);
+                accB.Z.v[q] = qs.ld(20 + q, i);
+                accB.T.v[q] = qs.ld(30 + q, i);
+            }
+        });
+#else
         pv_straus_xyz(X, Y, Z, at, bt, dig);
+#endif
         if (active) {
-            const Soa qs(wk.q, 40, wk.stride);
 #pragma unroll
             for (int q = 0; q < 10; q++) {
                 qs.st(q, i, X.v[q]);
@@ -1021,6 +1048,38 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
     }
 }
 
+// Straus path, [S]B of every Straus slot from the wide fixed-base comb (tiles from the end of the
+// slot range, like the other Straus kernels), extended, to q rows 0..39 for pv_msm_kernel.
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_straus_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
+                                                                   Gate gate) {
+    const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
+    if (blockIdx.x >= ntiles || nc >= n || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;
+    pv_straus_prio();
+    __shared__ uint4 stg[PV_BLOCK / 64][PV_BCOMB_STRIDE / 4][64];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Soa qs(wk.q, 40, wk.stride);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t sb = gate.stile(t, ntiles);
+        if ((sb + 1) * PV_BLOCK <= nc) break;
+        const uint32_t i0 = sb * PV_BLOCK + threadIdx.x;  // slot
+        const bool active = i0 < n && i0 >= nc;
+        const uint32_t i = active ? i0 : (uint32_t)n - 1;  // whole waves stay in step for the staging
+        const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
+        ge_p3 acc;
+        pv_comb_b_acc_w<PV_BC2_POS>(acc, DevB2Stage{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
+                                    [&](int j) { return dig.fb(j); });
+        if (active) {
+#pragma unroll
+            for (int q = 0; q < 10; q++) {
+                qs.st(q, i, acc.X.v[q]);
+                qs.st(10 + q, i, acc.Y.v[q]);
+                qs.st(20 + q, i, acc.Z.v[q]);
+                qs.st(30 + q, i, acc.T.v[q]);
+            }
+        }
+    }
+}
+
 // Wide fixed-base comb build (pv_init): each thread makes PV_BC2_RUN consecutive entries d0.. of one
 // row (base point P = [2^(W j)] B): start [d0] P by double-and-add, then P-steps, the projective
 // points parked in the entries themselves and the running product of their Z in `scratch`; one
@@ -1455,6 +1514,10 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_table_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#if PV_STRAUS_WIDE_B
+            hipLaunchKernelGGL(pv_straus_b_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, g_ctx.d_bc2, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#endif
             hipLaunchKernelGGL(pv_msm_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                g_ctx.d_btab, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -1480,6 +1543,11 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#if PV_STRAUS_WIDE_B
+            hipLaunchKernelGGL(pv_straus_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
+                               gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#endif
             if ((rc = mark(PV_STAGE_MSM))) return rc;
             hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                                g_ctx.d_btab, g_ctx.work, gate);

@@ -205,6 +205,39 @@ PV_HD void pv_straus_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const BTab& btab
     }
 }
 
+// Q = [k]A' + accB: the same regular-window loop over the radix-16 digits of k with the A table
+// only, then ONE cached addition of accB = [S]B (extended; the wide fixed-base comb, comb.h
+// pv_comb_b_acc_w). Drops the 32 interleaved B additions (32 x 7 products) for ~11 additions in
+// the comb plus the final one. load_accB(p) fetches accB only after the loop (no registers held).
+template <class ATab, class Dig, class AccB>
+PV_HD void pv_straus_a_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const Dig& dig, const AccB& load_accB) {
+    ge_p3 acc;
+    ge_p3_identity(acc);
+    ge_p1p1 t;
+    uint32_t ekw = 0;
+    for (int win = 63; win >= 0; win--) {
+        if ((win & 7) == 7) ekw = dig.ek(win >> 3);
+        const int e = pv_nibble(ekw, win);
+        if (win != 63) {
+            for (int j = 0; j < 3; j++) {
+                ge_p2_dbl(t, X, Y, Z);
+                ge_p1p1_to_p2(X, Y, Z, t);
+            }
+            ge_p2_dbl(t, X, Y, Z);
+            ge_p1p1_to_p3(acc, t);
+        }
+        pv_add_a(t, acc, atab, e);
+        if (win > 0) ge_p1p1_to_p2(X, Y, Z, t);
+    }
+    ge_p1p1_to_p3(acc, t);
+    ge_p3 accB;
+    load_accB(accB);
+    ge_cached cb;
+    ge_p3_to_cached(cb, accB);
+    ge_add_cached(t, acc, cb);
+    ge_p1p1_to_p2(X, Y, Z, t);
+}
+
 template <class ATab, class BTab, class Dig>
 PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const Dig& dig) {
     fe X, Y, Z;

@@ -251,6 +251,37 @@ int hc_sign_open_comb_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t* p
     return use[0] && pv_words_equal(enc[0], in.R);
 }
 
+// The Straus path with [S]B from the wide comb (PV_STRAUS_WIDE_B): checks, -A, k, the [j](-A)
+// table, pv_comb_b_acc_w<16> over the radix-65536 host table, pv_straus_a_xyz (loop over k only,
+// then one addition of [S]B), encoding.
+int hc_sign_open_straus_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    const std::vector<uint32_t>& bcomb = host_bcomb();
+    std::vector<uint8_t> buf(smlen + 256, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    ge_p3 negA;
+    uint32_t k[8];
+    HostMsg mw{buf.data()};
+    bool ok = pv_prepare(negA, k, in, smlen, mw);
+    HostATab at;
+    pv_build_a_table(at, negA);
+    pv_dig_regs dig;
+    sc_recode16(dig.e, k);
+    int32_t fb[16];
+    sc_recode_w<16, 16>(fb, in.S);
+    HostBRows brows{bcomb.data()};
+    ge_p3 accB;
+    pv_comb_b_acc_w<16>(accB, PvRowsStageB<HostBRows>{brows, 0, 0}, [&](int j) { return fb[j]; });
+    fe X, Y, Z;
+    pv_straus_a_xyz(X, Y, Z, at, dig, [&](ge_p3& p) { p = accB; });
+    uint32_t enc[8];
+    ge_p2_tobytes(enc, X, Y, Z);
+    return ok && pv_words_equal(enc, in.R);
+}
+
 // k = SHA-512(R||A||M) mod L through pv_prepare (exposes the hashing + reduction)
 void hc_prepare_k(uint8_t* kout, const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK

@@ -281,3 +281,19 @@ def test_wide_comb_path_vs_libsodium(hc, sodium, oracle):
         for _ in range(3):
             sm, pk = g.make(cls)
             assert bool(hc.hc_sign_open_comb_wide16(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
+
+
+def test_straus_wide_b_vs_libsodium(hc, sodium, oracle):
+    """The Straus path as the device runs it with PV_STRAUS_WIDE_B: the loop over k's radix-16 digits
+    with the [j](-A) table only, then one addition of [S]B from pv_comb_b_acc_w -- every golden
+    verdict and every adversarial class against libsodium."""
+    from vectors import VectorGen
+    with open(os.path.join(HERE, "golden", "verdicts.json")) as f:
+        for c in json.load(f):
+            sm, pk = bytes.fromhex(c["sm"]), bytes.fromhex(c["pk"])
+            assert bool(hc.hc_sign_open_straus_wide16(sm, ctypes.c_uint64(len(sm)), pk)) == c["ok"], c["cls"]
+    g = VectorGen(sodium, oracle, seed=24)
+    for cls in VectorGen.CLASSES:
+        for _ in range(3):
+            sm, pk = g.make(cls)
+            assert bool(hc.hc_sign_open_straus_wide16(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
