@@ -135,7 +135,10 @@ int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* laun
  * with 32 additions from the key's radix-256 comb table (660 KB of HBM per key, built once by the
  * engine's key-chain and fill kernels) instead of 252 doublings + 64 additions; verdicts are
  * unchanged (the table holds exact multiples of -A, and libsodium's key checks ran when it was built).
- * The throughput paths (and so the benchmark's headline) never read it.
+ * Above the latency path's range (AUTO: batches > 4,096 requests) a non-empty cache also makes the
+ * launch keyed at any size: a cached key's requests take the comb path at any request count and its
+ * table is read from the cache instead of being built (no key chain / table fill for it); uncached
+ * keys are handled as without the cache. The benchmark's headline never configures it.
  *   pv_key_cache_configure(capacity)  allocate room for `capacity` keys (0 = free, disabled)
  *   pv_key_cache_put(pks, n)          host keys (n x 32 B): build and insert the missing ones, refresh
  *                                     the present ones; least recently put keys are evicted when full.
