@@ -50,7 +50,15 @@ static constexpr int PV_BLOCK = 256;
 #endif
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
-static constexpr uint64_t PV_KEYED_MIN = 32768;   // AUTO: smaller chunks skip dedup (Straus only)
+// AUTO: chunks above the latency path's range go keyed (dedup, then comb keys / Straus side). At
+// medium sizes (4k-256k requests) the Straus side's one-lane latency (~0.9 ms) is paid by the whole
+// launch as soon as it has any request, so a chunk with few distinct keys makes EVERY key a comb
+// key (PV_ALLCOMB_*): tools/latency_probe.py on MI355X, 1,024 signers, device time per call --
+// 10k requests 0.77 ms all-comb vs 0.91 Straus, 32k 0.76 vs 0.95 (and 1.02 split at >= 48 requests
+// per key); bounded so the fill never exceeds 2,048 keys' tables (~0.5 ms).
+static constexpr uint64_t PV_KEYED_MIN = 4097;
+static constexpr uint32_t PV_ALLCOMB_KEYS = 2048;
+static constexpr uint32_t PV_ALLCOMB_CHUNK = 262144;
 #ifndef PV_LP_CHAIN_BLOCKS
 #define PV_LP_CHAIN_BLOCKS 2048  // waves of the limb-parallel key chain (one key each at a time)
 #endif
@@ -274,7 +282,8 @@ struct KeyWork {
     uint32_t kcap;
     uint32_t seed;
     uint32_t min_req;
-    uint32_t kc_on;  // this launch consults the key cache (pv_key_cache_probe_kernel ran)
+    uint32_t kc_on;    // this launch consults the key cache (pv_key_cache_probe_kernel ran)
+    uint32_t chunk_n;  // requests in this chunk
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 #ifndef PV_COMB_MIN_REQ
@@ -541,9 +550,11 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
     const uint32_t t = threadIdx.x;
     const uint32_t per = (nk + 1023) / 1024;
     const uint32_t lo = min(t * per, nk), hi = min(lo + per, nk);
-    // a key in the node-side cache costs no table build: it is a comb candidate at any count
+    // a key in the node-side cache costs no table build: it is a comb candidate at any count; a
+    // medium chunk with few distinct keys makes every key a comb key (PV_ALLCOMB_*)
+    const bool all_comb = nk <= PV_ALLCOMB_KEYS && kw.chunk_n <= PV_ALLCOMB_CHUNK;
     auto is_cand = [&](uint32_t id, uint32_t c) {
-        return c >= kw.min_req || (kw.kc_on && kw.key_cslot[id] != PV_EMPTY);
+        return all_comb || c >= kw.min_req || (kw.kc_on && kw.key_cslot[id] != PV_EMPTY);
     };
     uint32_t cand = 0;
     for (uint32_t id = lo; id < hi; id++) cand += is_cand(id, kw.key_count[id]) ? 1u : 0u;
@@ -1439,19 +1450,18 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         // path (~3 vs ~13 ns), so AUTO gives a table to keys with >= PV_COMB_MIN_REQ requests in
         // the chunk and verifies every other request on the Straus path in the same launch. The
         // split is computed on the device by the dedup/sort kernels (Gate); nothing synchronises.
-        // Chunks below PV_KEYED_MIN requests skip dedup (~0.3 ms of fixed work) and go Straus --
-        // unless the node-side key cache holds keys: a cached key's comb table is already built, so
-        // any chunk above the latency path's range goes keyed and its cached keys' requests take
-        // the comb path at any count (48 table additions instead of the Straus loop).
+        // Chunks below PV_KEYED_MIN (the latency path's range; only the tail chunk of a large
+        // batch can be that small) skip dedup and go Straus. A key in the node-side key cache has
+        // its comb table already built: its requests take the comb path at any count.
         const PvKeyCacheView kcv = kc_view();
         const bool kc_active = kcv.hmask != 0;
-        const bool keyed = g_ctx.path == PV_PATH_COMB ||
-                           (g_ctx.path == PV_PATH_AUTO && (m >= PV_KEYED_MIN || (kc_active && m > PV_LATENCY_MAX)));
+        const bool keyed = g_ctx.path == PV_PATH_COMB || (g_ctx.path == PV_PATH_AUTO && m >= PV_KEYED_MIN);
         Gate gate{nullptr, nullptr};
         g_ctx.last_keyed = keyed;
         KeyWork kw = g_ctx.kw;
         kw.min_req = g_ctx.path == PV_PATH_COMB ? 1u : (uint32_t)PV_COMB_MIN_REQ;
         kw.kc_on = kc_active ? 1u : 0u;
+        kw.chunk_n = (uint32_t)m;
         kw.kc_tab = g_ctx.kc.d_tab;
         const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
         if (keyed) {

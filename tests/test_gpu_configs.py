@@ -265,3 +265,28 @@ def test_split_all_keys_distinct(native, sodium):
     got = native.verify_sm_batch(blob, off, pks)
     assert native.last_split() == (40000, 0, 0)
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+
+
+def test_medium_chunks_all_comb_or_split(native, sodium):
+    """AUTO at medium sizes: a 20k chunk with few distinct keys (1,024 signers + 600 one-off keys)
+    makes every key a comb key, one-request keys included; a 20k chunk with more than 2,048
+    distinct keys keeps the >= 48-requests rule (the 1,024 signers' ~19 requests each stay Straus
+    side). Both bit-exact against libsodium, as are the forced paths."""
+    from oracle.oracle import cpu_verdicts
+    for n_signed, n_single, want_all in ((19456, 600, True), (12288, 4000, False)):
+        blob, off, pks = _split_batch(sodium, n_signed, n_single, seed=13 + n_single)
+        n = len(off) - 1
+        want = cpu_verdicts(blob, off, pks)
+        got = native.verify_sm_batch(blob, off, pks)
+        keys_all, comb_keys, comb_req = native.last_split()
+        assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+        assert keys_all == 1024 + n_single, keys_all
+        if want_all:
+            assert (comb_keys, comb_req) == (keys_all, n), (comb_keys, comb_req)
+        else:
+            assert comb_keys == 0 and comb_req == 0, (comb_keys, comb_req)
+        for path in (native.PV_PATH_COMB, native.PV_PATH_STRAUS):
+            native.set_path(path)
+            got = native.verify_sm_batch(blob, off, pks)
+            native.set_path(native.PV_PATH_AUTO)
+            assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])

@@ -131,7 +131,7 @@ def test_cached_keys_on_keyed_path(nat, sodium, oracle):
     got = nat.verify_sm_batch(blob, off, pks)
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
     path, nkeys = nat.last_path()
-    assert path == nat.PV_PATH_COMB  # keyed although the batch is below the dedup threshold
+    assert path == nat.PV_PATH_COMB
     keys_all, comb_keys, comb_req = nat.last_split()
     # every cached key (30 signers + the bad keys) plus the 10 uncached signers with ~300 requests
     assert comb_keys >= 30 + 10, (keys_all, comb_keys, comb_req)
@@ -146,7 +146,9 @@ def test_cached_keys_on_keyed_path(nat, sodium, oracle):
     assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
     kc.enable(False)
     assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
-    assert nat.last_path()[0] == nat.PV_PATH_STRAUS  # below the dedup threshold without the cache
+    # without the cache: a medium chunk with few distinct keys makes every key a comb key
+    keys_all, comb_keys, comb_req = nat.last_split()
+    assert keys_all <= 2048 and comb_keys == keys_all and comb_req == len(cases), (keys_all, comb_keys, comb_req)
     kc.enable(True)
     kc.clear()
     assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
