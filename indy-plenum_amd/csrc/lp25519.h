@@ -490,6 +490,29 @@ LP_FN lu lp_ext_from_xy(const LpLane& c, const LpConsts& K, const lu& X, const l
     return lp_mul(c, c.rows(x, y, K.one, x), c.rows(K.one, K.one, K.one, y));
 }
 
+// The comb key chain (comb.h pv_comb_chain) over positions [lo, hi): P = P_lo = [256^lo](-A) on
+// entry; store(i, m, P) receives slot m of position i (P_i, then its [16], [32], [64] multiples);
+// returns P_hi for the next part (hi < 32). pv_key_chain_lp_kernel runs the 32 positions in parts so
+// that the table fill of a part overlaps the chain of the next.
+template <class Store>
+LP_FN lu lp_comb_chain_part(const LpLane& c, lu P, int lo, int hi, const Store& store) {
+    for (int i = lo; i < hi; i++) {
+        store(i, 0, P);
+        const int nd = i + 1 < 32 ? 8 : 6;
+        for (int j = 0; j < nd; j++) {
+            P = lp_dbl(c, P);
+            if (j >= 3 && j <= 5) store(i, j - 2, P);
+        }
+    }
+    return P;
+}
+// An extended point back from its 40 stored words (X, Y, Z, T, 10 carried limbs each): lane
+// 16 r + k <- word 10 r + k, the scratch lanes 10..15 of a row 0. A stored point is a valid lp
+// operand (carried limbs, consistent T), so a chain part resumes from the previous part's P_hi.
+LP_FN lu lp_load_ext40(const LpLane& c, const uint32_t* w) {
+    return lp_sel(c.kge10, 0u, lp_gather(w, lp_sel(c.kge10, 0u, c.row * 10u + c.k)));
+}
+
 // The table of [j](-A), j = -8..8, cached form, for the signed radix-16 digits of k. store(j, q).
 template <class Store>
 LP_FN void lp_build_a_table(const LpLane& c, const LpConsts& K, const lu& negA, const Store& store) {

@@ -59,6 +59,14 @@ static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tabl
 static constexpr uint64_t PV_KEYED_MIN = 4097;
 static constexpr uint32_t PV_ALLCOMB_KEYS = 2048;
 static constexpr uint32_t PV_ALLCOMB_CHUNK = 262144;
+// Key chain launches per keyed chunk (the table fill of part p overlaps the chain of part p + 1).
+// A/B on MI355X (profiles/r02/ab_chain_parts.txt, interleaved): 1 part is best -- 10k requests
+// 0.70 ms device vs 0.74 (4 parts) / 0.92 (8), 1M 3.02 ms/step vs 3.04-3.11 / 3.15: the fill of a
+// part competes with the next chain part for the SIMDs and each part is a launch of its own.
+#ifndef PV_CHAIN_PARTS
+#define PV_CHAIN_PARTS 1
+#endif
+static_assert(32 % PV_CHAIN_PARTS == 0, "PV_CHAIN_PARTS must divide the 32 comb positions");
 #ifndef PV_LP_CHAIN_BLOCKS
 #define PV_LP_CHAIN_BLOCKS 2048  // waves of the limb-parallel key chain (one key each at a time)
 #endif
@@ -890,16 +898,10 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const ui
 }
 
 #if LP_DEVICE
+// Positions [lo, hi) of one key's chain. Part 0 decompresses -A and writes the key flag; a later part
+// resumes from P_lo, which the previous part stored as slot 0 of position lo.
 __device__ __forceinline__ void pv_key_chain_lp(const uint8_t* __restrict__ pk, const KeyWork& kw, uint32_t id,
-                                                const LpLane& c, const LpConsts& K) {
-    uint32_t A[8];
-    pv_load_pk(A, pk, kw.key_owner[kw.comb_key[id]]);
-    lu sw[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) sw[q] = A[q];
-    const LpDecomp dec = lp_decompress_ar(c, K, sw);
-    const bool ok = pv_ge_is_canonical(A) && !pv_has_small_order(A) && dec.ok_a;
-    if (threadIdx.x == 0) kw.key_flag[id] = ok ? 1u : 0u;
+                                                const LpLane& c, const LpConsts& K, int lo, int hi) {
     uint32_t* b = reinterpret_cast<uint32_t*>(kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10);
     const uint32_t w = 10u * (threadIdx.x >> 4) + (threadIdx.x & 15u);  // word of [X, Y, Z, T] x 10 limbs
     const bool limb = (threadIdx.x & 15u) < 10u;
@@ -907,15 +909,22 @@ __device__ __forceinline__ void pv_key_chain_lp(const uint8_t* __restrict__ pk, 
         const lu R = lp_carry1(c, P);  // LR -> limb < 2^w + 19: the per-lane code's reduced bound
         if (limb) b[(i * PV_COMB_PTS + m) * 40 + w] = R;
     };
-    lu P = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
-    for (int i = 0; i < PV_COMB_POS; i++) {
-        store(i, 0, P);
-        const int nd = i + 1 < PV_COMB_POS ? 8 : 6;
-        for (int j = 0; j < nd; j++) {
-            P = lp_dbl(c, P);
-            if (j >= 3 && j <= 5) store(i, j - 2, P);
-        }
+    lu P;
+    if (lo == 0) {
+        uint32_t A[8];
+        pv_load_pk(A, pk, kw.key_owner[kw.comb_key[id]]);
+        lu sw[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) sw[q] = A[q];
+        const LpDecomp dec = lp_decompress_ar(c, K, sw);
+        const bool ok = pv_ge_is_canonical(A) && !pv_has_small_order(A) && dec.ok_a;
+        if (threadIdx.x == 0) kw.key_flag[id] = ok ? 1u : 0u;
+        P = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
+    } else {
+        P = lp_load_ext40(c, b + lo * PV_COMB_PTS * 40);
     }
+    P = lp_comb_chain_part(c, P, lo, hi, store);
+    if (hi < PV_COMB_POS) store(hi, 0, P);  // P_hi: where the next part resumes
 }
 #endif
 
@@ -926,7 +935,8 @@ __device__ __forceinline__ void pv_key_chain_lp(const uint8_t* __restrict__ pk, 
 // companion kernel: a gated launch is not free on a saturated chip, its blocks wait ~0.2 ms for
 // dispatch slots (rocprofv3, profiles/r02/prof_a). Same outputs as pv_key_chain_quad_kernel: key_flag
 // and the bases [256^i](-A) with their [16], [32], [64] multiples, carried to reduced limbs.
-__global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __restrict__ pk, KeyWork kw, Gate gate) {
+__global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __restrict__ pk, KeyWork kw, Gate gate,
+                                                              int lo, int hi) {
 #if LP_DEVICE
     if (!gate.keyed()) return;
     const uint32_t nk = kw.nkeys[PV_SPLIT_COMB_KEYS];
@@ -935,18 +945,21 @@ __global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __re
     const LpLane c = LpLane::make();
     const LpConsts K = LpConsts::make(c);
     for (uint32_t id = blockIdx.x; id < nk; id += gridDim.x)
-        if (kw.comb_cslot[id] == PV_EMPTY) pv_key_chain_lp(pk, kw, id, c, K);  // cached: table ready
+        if (kw.comb_cslot[id] == PV_EMPTY) pv_key_chain_lp(pk, kw, id, c, K, lo, hi);  // cached: table ready
 #endif
 }
 
-// Per (key, position, block of 16 entries): the comb table rows. Grid-stride over nkeys * 256 items.
-__global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kernel(KeyWork kw, Gate gate) {
+// Per (key, position in [lo, hi), block of 16 entries): the comb table rows. Grid-stride over
+// nkeys * (hi - lo) * 8 items.
+__global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kernel(KeyWork kw, Gate gate, int lo,
+                                                                                  int hi) {
     if (!gate.keyed()) return;
-    const uint32_t items = kw.nkeys[PV_SPLIT_COMB_KEYS] * PV_COMB_POS * PV_COMB_BLOCKS;
+    const uint32_t np = (uint32_t)(hi - lo);
+    const uint32_t items = kw.nkeys[PV_SPLIT_COMB_KEYS] * np * PV_COMB_BLOCKS;
     for (uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x; it < items; it += gridDim.x * PV_BLOCK) {
-        const uint32_t id = it / (PV_COMB_POS * PV_COMB_BLOCKS);
+        const uint32_t id = it / (np * PV_COMB_BLOCKS);
         if (kw.comb_cslot[id] != PV_EMPTY) continue;  // the key's table is in the node-side cache
-        const int pos = (it / PV_COMB_BLOCKS) % PV_COMB_POS;
+        const int pos = lo + (int)((it / PV_COMB_BLOCKS) % np);
         const int b = it % PV_COMB_BLOCKS;
         const DevBasePts pts{DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10}, pos};
         pv_comb_fill_block(DevCombRow{kw.ctab + ((uint64_t)id * PV_COMB_POS + pos) * PV_COMB_ENT * 10}, pts, b);
@@ -1264,7 +1277,9 @@ struct Ctx {
     hipStream_t stream = nullptr;
     hipStream_t kstream = nullptr;           // per-key pipeline (chain + table fill), overlapped
     hipEvent_t ev_keys_ready = nullptr;      // dedup done (main -> kstream)
-    hipEvent_t ev_tables_ready = nullptr;    // comb tables done (kstream -> main)
+    hipEvent_t ev_tables_ready = nullptr;    // comb tables done (fstream -> main)
+    hipStream_t fstream = nullptr;           // table fill, one launch per chain part
+    hipEvent_t ev_chain[PV_CHAIN_PARTS] = {};  // chain part done (kstream -> fstream)
     hipStream_t sstream = nullptr;           // Straus-path slots of a split chunk, overlapped
     hipEvent_t ev_straus_done = nullptr;     // their q / flags written (sstream -> main)
     // Workspace hand-over between callers' streams: every launch ends by recording ev_launch_done
@@ -1487,22 +1502,34 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             // overlapped with the per-request prep on the main stream
             PV_HIP(hipEventRecord(g_ctx.ev_keys_ready, stream), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(g_ctx.kstream, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
+            // the chain runs in PV_CHAIN_PARTS launches of consecutive positions; the fill of a part
+            // runs on fstream as soon as its chain part is done, beside the chain of the next part
 #if PV_CHAIN_MODE == 2
-            hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(limit, PV_LP_CHAIN_BLOCKS)), dim3(64), 0,
-                               g_ctx.kstream, d_pk + 32 * c0, kw, gate);
-#elif PV_CHAIN_MODE == 1
-            hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK),
-                               0, g_ctx.kstream, d_pk + 32 * c0, kw, gate);
+            constexpr int parts = PV_CHAIN_PARTS;
 #else
-            hipLaunchKernelGGL(pv_key_chain_kernel, dim3((limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
-                               g_ctx.kstream, d_pk + 32 * c0, kw, gate);
+            constexpr int parts = 1;
 #endif
-            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            const uint64_t items = (uint64_t)limit * PV_COMB_POS * PV_COMB_BLOCKS;
+            const uint64_t items = (uint64_t)limit * (PV_COMB_POS / parts) * PV_COMB_BLOCKS;
             const unsigned fgrid = (unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096);
-            hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, g_ctx.kstream, kw, gate);
-            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.kstream), PV_ERR_LAUNCH);
+            for (int part = 0; part < parts; part++) {
+                const int lo = part * PV_COMB_POS / parts, hi = (part + 1) * PV_COMB_POS / parts;
+#if PV_CHAIN_MODE == 2
+                hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(limit, PV_LP_CHAIN_BLOCKS)), dim3(64),
+                                   0, g_ctx.kstream, d_pk + 32 * c0, kw, gate, lo, hi);
+#elif PV_CHAIN_MODE == 1
+                hipLaunchKernelGGL(pv_key_chain_quad_kernel, dim3((4 * limit + PV_BLOCK - 1) / PV_BLOCK),
+                                   dim3(PV_BLOCK), 0, g_ctx.kstream, d_pk + 32 * c0, kw, gate);
+#else
+                hipLaunchKernelGGL(pv_key_chain_kernel, dim3((limit + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0,
+                                   g_ctx.kstream, d_pk + 32 * c0, kw, gate);
+#endif
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+                PV_HIP(hipEventRecord(g_ctx.ev_chain[part], g_ctx.kstream), PV_ERR_LAUNCH);
+                PV_HIP(hipStreamWaitEvent(g_ctx.fstream, g_ctx.ev_chain[part], 0), PV_ERR_LAUNCH);
+                hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, g_ctx.fstream, kw, gate, lo, hi);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            }
+            PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
         }
         if ((rc = mark(PV_STAGE_PREP))) return rc;
         if (keyed) {
@@ -1613,6 +1640,8 @@ int pv_init(int device) {
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.kstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_keys_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipStreamCreateWithFlags(&g_ctx.fstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+    for (auto& e : g_ctx.ev_chain) PV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
@@ -1736,6 +1765,9 @@ void pv_shutdown(void) {
     if (g_ctx.kstream) (void)hipStreamDestroy(g_ctx.kstream);
     if (g_ctx.ev_keys_ready) (void)hipEventDestroy(g_ctx.ev_keys_ready);
     if (g_ctx.ev_tables_ready) (void)hipEventDestroy(g_ctx.ev_tables_ready);
+    if (g_ctx.fstream) (void)hipStreamDestroy(g_ctx.fstream);
+    for (hipEvent_t e : g_ctx.ev_chain)
+        if (e) (void)hipEventDestroy(e);
     if (g_ctx.sstream) (void)hipStreamDestroy(g_ctx.sstream);
     if (g_ctx.ev_straus_done) (void)hipEventDestroy(g_ctx.ev_straus_done);
     if (g_ctx.ev_launch_done) (void)hipEventDestroy(g_ctx.ev_launch_done);
@@ -2047,11 +2079,11 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
         PV_HIP(hipMemsetAsync(kw.comb_cslot, 0xFF, (uint64_t)m * 4, s), PV_ERR_LAUNCH);  // build every table
         const Gate gate{kw.nkeys, kw.slot_req};
         hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(m, PV_LP_CHAIN_BLOCKS)), dim3(64), 0, s,
-                           k.d_put_pk, kw, gate);
+                           k.d_put_pk, kw, gate, 0, PV_COMB_POS);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         const uint64_t items = (uint64_t)m * PV_COMB_POS * PV_COMB_BLOCKS;
         hipLaunchKernelGGL(pv_key_fill_kernel, dim3((unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096)),
-                           dim3(PV_BLOCK), 0, s, kw, gate);
+                           dim3(PV_BLOCK), 0, s, kw, gate, 0, PV_COMB_POS);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         hipLaunchKernelGGL(pv_kc_scatter_kernel, dim3(64, m), dim3(PV_BLOCK), 0, s, kw.ctab, kw.key_flag, k.d_put_pk,
                            k.d_put_slot, m, k.d_tab, k.d_flags, k.d_keys);

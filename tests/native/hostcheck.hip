@@ -462,4 +462,56 @@ int hc_lp_chain_check(const uint8_t* pk) {
     return bad;
 }
 
+// The chain as pv_key_chain_lp_kernel runs it with PV_CHAIN_PARTS = parts: lp_comb_chain_part per
+// part, every point stored as its 40 carried words, and each later part resuming from the stored
+// P_lo (lp_load_ext40). Returns the number of stored points that differ from pv_comb_chain's (as
+// affine points) or whose T is inconsistent.
+int hc_lp_chain_parts_check(const uint8_t* pk, int parts) {
+    uint32_t A[8];
+    memcpy(A, pk, 32);
+    ge_p3 negA;
+    if (!pv_key_ok_negate(negA, A)) return -1;
+    std::vector<ge_p3> ref(PV_COMB_POS * PV_COMB_PTS);
+    pv_comb_chain(HostBases{ref.data()}, negA);
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    lu sw[8];
+    for (int q = 0; q < 8; q++) sw[q] = A[q];
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    std::vector<uint32_t> b(PV_COMB_POS * PV_COMB_PTS * 40, 0xDEADBEEFu);
+    auto store = [&](int i, int m, const lu& P) {
+        const lu R = lp_carry1(c, P);
+        for (int l = 0; l < 64; l++)
+            if ((l & 15) < 10) b[(i * PV_COMB_PTS + m) * 40 + 10 * (l >> 4) + (l & 15)] = R.v[l];
+    };
+    for (int part = 0; part < parts; part++) {
+        const int lo = part * PV_COMB_POS / parts, hi = (part + 1) * PV_COMB_POS / parts;
+        lu P = lo == 0 ? lp_ext_from_xy(c, K, dec.X, dec.Y, 0) : lp_load_ext40(c, b.data() + lo * PV_COMB_PTS * 40);
+        P = lp_comb_chain_part(c, P, lo, hi, store);
+        if (hi < PV_COMB_POS) store(hi, 0, P);
+    }
+    int bad = 0;
+    for (int i = 0; i < PV_COMB_POS; i++)
+        for (int m = 0; m < PV_COMB_PTS; m++) {
+            fe X, Y, Z, T;
+            memcpy(X.v, &b[(i * PV_COMB_PTS + m) * 40], 40);
+            memcpy(Y.v, &b[(i * PV_COMB_PTS + m) * 40 + 10], 40);
+            memcpy(Z.v, &b[(i * PV_COMB_PTS + m) * 40 + 20], 40);
+            memcpy(T.v, &b[(i * PV_COMB_PTS + m) * 40 + 30], 40);
+            for (const fe* f : {&X, &Y, &Z, &T}) fe_check_reduced(*f);
+            const ge_p3& r = ref[i * PV_COMB_PTS + m];
+            fe a1, a2, zi, t;
+            uint32_t u[8], v[8];
+            // X / Z == r.X / r.Z and Y / Z == r.Y / r.Z, cross-multiplied
+            fe_mul(a1, X, r.Z); fe_mul(a2, r.X, Z); fe_tobytes32(u, a1); fe_tobytes32(v, a2);
+            if (memcmp(u, v, sizeof u)) bad++;
+            fe_mul(a1, Y, r.Z); fe_mul(a2, r.Y, Z); fe_tobytes32(u, a1); fe_tobytes32(v, a2);
+            if (memcmp(u, v, sizeof u)) bad++;
+            fe_mul(a1, X, Y); fe_mul(a2, T, Z); fe_tobytes32(u, a1); fe_tobytes32(v, a2);
+            if (memcmp(u, v, sizeof u)) bad++;
+            (void)zi; (void)t;
+        }
+    return bad;
+}
+
 }  // extern "C"

@@ -166,3 +166,16 @@ def test_lp_key_chain_matches_per_lane_chain(hc, oracle):
     keys.append(oracle.point_add(keys[0], ORDER8))  # mixed-order key
     for pk in keys:
         assert hc.hc_lp_chain_check(pk) == 0
+
+
+def test_lp_key_chain_in_parts(hc, oracle):
+    """The chain as the keyed launch runs it (PV_CHAIN_PARTS launches, each resuming from the previous
+    part's stored, carried P_lo) stores the same points as the per-lane chain, with consistent T,
+    for 1, 2, 4 and 8 parts."""
+    rng = random.Random(9)
+    from vectors import ORDER8
+    keys = [oracle.scalarmult_base(rng.randrange(1, L).to_bytes(32, "little")) for _ in range(2)]
+    keys.append(oracle.point_add(keys[0], ORDER8))
+    for pk in keys:
+        for parts in (1, 2, 4, 8):
+            assert hc.hc_lp_chain_parts_check(pk, parts) == 0, parts
