@@ -18,6 +18,8 @@
 #include <mutex>
 #include <random>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <thread>
 #include <string>
 #include <vector>
@@ -1853,32 +1855,94 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
     return launch(d_sm, d_off, n, d_pk, d_verdict_words, stream ? (hipStream_t)stream : g_ctx.stream);
 }
 
-// Move the request blob host -> pinned staging -> HBM. One host thread copies ~10 GB/s and the blob of
-// a large host-buffer batch is hundreds of MB, so up to 8 threads each take a contiguous slice and
-// copy it in 4 MB pieces, enqueueing each piece's DMA (hipMemcpyAsync from pinned memory) as soon as
-// it is staged: the PCIe transfer of earlier pieces overlaps the staging copy of later ones. The
-// pieces are disjoint, so their order on the stream does not matter; the kernels launched on the
-// same stream afterwards see every piece.
-static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* src, uint64_t bytes, hipStream_t s) {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const unsigned nt = bytes < (8ull << 20) ? 1u : std::min(8u, hw);
-    const uint64_t piece = 4ull << 20;
-    std::atomic<int> err{0};
-    auto work = [&](uint64_t a, uint64_t b) {
-        for (uint64_t o = a; o < b; o += piece) {
-            const uint64_t e = std::min(b, o + piece);
-            memcpy(h_stage + o, src + o, e - o);
-            if (hipMemcpyAsync(d_dst + o, h_stage + o, e - o, hipMemcpyHostToDevice, s) != hipSuccess) err = 1;
+// Host-side copy pool for the host-buffer entry: persistent threads (created on first use, at most 8,
+// half the host's hardware threads), so a call pays no thread creation. run(k, fn) executes fn(0..k-1)
+// on the pool and the calling thread and returns when all are done. Used under g_mu only.
+class CopyPool {
+   public:
+    void run(unsigned k, const std::function<void(unsigned)>& fn) {
+        if (k <= 1 || workers() == 0) {
+            for (unsigned i = 0; i < k; i++) fn(i);
+            return;
         }
-    };
-    const uint64_t per = (bytes + nt - 1) / nt;
-    std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt; t++) {
-        const uint64_t a = std::min<uint64_t>(bytes, t * per), b = std::min<uint64_t>(bytes, a + per);
-        if (b > a) th.emplace_back(work, a, b);
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &fn;
+            next_ = 0;
+            total_ = k;
+            done_ = 0;
+            gen_++;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return done_ == total_; });
+        fn_ = nullptr;
     }
-    work(0, std::min<uint64_t>(bytes, per));
-    for (auto& x : th) x.join();
+
+   private:
+    unsigned workers() {
+        if (!started_) {
+            started_ = true;
+            const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+            const unsigned nw = std::min(8u, hw / 2);
+            for (unsigned i = 0; i + 1 < nw; i++) th_.emplace_back([this] { loop(); });
+        }
+        return (unsigned)th_.size();
+    }
+    void drain() {  // take tasks until none is left
+        for (;;) {
+            unsigned i;
+            const std::function<void(unsigned)>* f;
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                if (!fn_ || next_ >= total_) return;
+                i = next_++;
+                f = fn_;
+            }
+            (*f)(i);
+            std::lock_guard<std::mutex> lk(m_);
+            if (++done_ == total_) done_cv_.notify_all();
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+            }
+            drain();
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(unsigned)>* fn_ = nullptr;
+    unsigned next_ = 0, total_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+    bool started_ = false;
+    std::vector<std::thread> th_;
+};
+// never destroyed: its threads sleep on the condition variable until the process ends (a forked child,
+// which has none of them, must not run a destructor that joins them)
+CopyPool& g_copy_pool = *new CopyPool;
+
+// Move the request blob host -> pinned staging -> HBM. One host thread copies ~10 GB/s, so the blob is
+// cut into pieces (256 KB - 4 MB) that the copy pool stages in parallel; with `dma`, each piece's DMA
+// (hipMemcpyAsync from pinned memory) is enqueued as soon as it is staged, so the PCIe transfer of
+// earlier pieces overlaps the staging of later ones (the pieces are disjoint: their order on the
+// stream does not matter, and the kernels launched on the same stream afterwards see every piece).
+static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* src, uint64_t bytes, hipStream_t s,
+                              bool dma) {
+    const uint64_t piece = std::min<uint64_t>(4ull << 20, std::max<uint64_t>(256ull << 10, bytes / 16));
+    const unsigned k = (unsigned)((bytes + piece - 1) / piece);
+    std::atomic<int> err{0};
+    g_copy_pool.run(k, [&](unsigned i) {
+        const uint64_t o = (uint64_t)i * piece, e = std::min(bytes, o + piece);
+        memcpy(h_stage + o, src + o, e - o);
+        if (dma && hipMemcpyAsync(d_dst + o, h_stage + o, e - o, hipMemcpyHostToDevice, s) != hipSuccess) err = 1;
+    });
     return err.load() ? fail(PV_ERR_LAUNCH, "hipMemcpyAsync (request blob) failed") : PV_OK;
 }
 
@@ -1900,9 +1964,17 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     int rc = ensure_stage(total, total);
     if (rc) return rc;
     uint8_t* h = g_ctx.h_stage;
-    memcpy(h, pk, n * 32);
     uint64_t* hoff = reinterpret_cast<uint64_t*>(h + pk_bytes);
-    for (uint64_t i = 0; i <= n; i++) hoff[i] = sm_off[i] - sm_off[0];
+    {  // keys and rebased offsets, in parallel slices for large batches
+        const uint64_t base = sm_off[0];
+        const unsigned k = n >= (1u << 16) ? 8u : 1u;
+        g_copy_pool.run(k, [&](unsigned t) {
+            const uint64_t a = n * t / k, b = n * (t + 1) / k;
+            memcpy(h + 32 * a, pk + 32 * a, 32 * (b - a));
+            for (uint64_t i = a; i < b; i++) hoff[i] = sm_off[i] - base;
+        });
+        hoff[n] = sm_off[n] - base;
+    }
     uint8_t* hblob = h + pk_bytes + off_bytes + v_bytes;
     memset(hblob + blob, 0, PV_BLOB_SLACK);
     uint8_t* d = g_ctx.d_stage;
@@ -1910,14 +1982,19 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     hipStream_t s = g_ctx.stream;
     // the verdict words travel zeroed (the latency path ORs its bits into them)
     memset(h + pk_bytes + off_bytes, 0, v_bytes);
-    if (blob < (8ull << 20)) {
+    if (blob < (256ull << 10)) {
         // small batch (Plenum's quotas): one copy of the whole staging area, one DMA
         memcpy(hblob, sm + sm_off[0], blob);
+        PV_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    } else if (blob < (8ull << 20)) {
+        // medium: the blob staged by the copy pool, then one DMA of the whole staging area
+        rc = pv_stage_to_device(dblob, hblob, sm + sm_off[0], blob, s, false);
+        if (rc) return rc;
         PV_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
     } else {
         PV_HIP(hipMemcpyAsync(d, h, pk_bytes + off_bytes + v_bytes, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemcpyAsync(dblob + blob, hblob + blob, PV_BLOB_SLACK, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-        rc = pv_stage_to_device(dblob, hblob, sm + sm_off[0], blob, s);
+        rc = pv_stage_to_device(dblob, hblob, sm + sm_off[0], blob, s, true);
         if (rc) {
             (void)hipStreamSynchronize(s);  // no DMA may still read the staging buffer when the caller retries
             return rc;
