@@ -1699,7 +1699,11 @@ int pv_init(int device) {
         // the wide fixed-base comb, built on the device row by row (one scratch row of Z products)
         {
             const uint64_t rows_ent = (uint64_t)(PV_BC2_POS - 1) * PV_BC2_ENT + PV_BC2_TOP_ENT;
-            PV_HIP(hipMalloc((void**)&g_ctx.d_bc2, rows_ent * PV_BCOMB_STRIDE * 4), PV_ERR_ALLOC);
+            if (hipMalloc((void**)&g_ctx.d_bc2, rows_ent * PV_BCOMB_STRIDE * 4) != hipSuccess)
+                return fail(PV_ERR_ALLOC, "pv_init: cannot allocate the wide fixed-base comb (" +
+                                              std::to_string(rows_ent * PV_BCOMB_STRIDE * 4 >> 20) +
+                                              " MiB of HBM at radix 2^" + std::to_string(PV_BC2_W) +
+                                              "); rebuild with EXTRA=-DPV_BCOMB_W=20 (805 MiB) or 16 (67 MiB)");
             uint32_t* scratch = nullptr;
             PV_HIP(hipMalloc((void**)&scratch, (uint64_t)PV_BC2_ENT * 40), PV_ERR_ALLOC);
             ge_p3 negB, P;
