@@ -97,6 +97,90 @@ PV_HD void pv_comb_fill_block(const Table& tab, const Pts& pts, int b) {
     }
 }
 
+// Sparse fill of one position's row for a small chunk (a few requests per key, AUTO all-comb): only
+// the entries the chunk's digits use are built. Always: T[0..16] (the identity and [r] P, r < 16, by
+// P-steps) and T[16 q], q = 1..8 (from the chain's [16], [32], [64] P: 5 additions); then every other
+// needed entry d = 16 q + r as ONE addition T[16 q] + T[r] (T[16 q] back to extended from its cached
+// words: X = (y+x) - (y-x), Y = (y+x) + (y-x), Z = 2Z, T = 2dT / d, i.e. the point times 2). About 20 +
+// (needed) additions per position instead of 129. need.word(w) = bits 32 w .. 32 w + 31 of the
+// position's needed |digit| set; row.load(d, c) reads back a stored entry.
+static constexpr uint32_t PV_SPARSE_PRE[5] = {0x0001FFFFu, 0x00010001u, 0x00010001u, 0x00010001u, 0x1u};
+template <class Row, class Pts, class Need>
+PV_HD void pv_comb_fill_sparse(const Row& row, const Pts& pts, const Need& need) {
+    ge_p3 P, cur;
+    pts.load(0, P);
+    ge_cached cP, c;
+    ge_p3_to_cached(cP, P);
+    ge_p1p1 t;
+    ge_cached_identity(c);
+    row.store(0, c);
+    row.store(1, cP);
+    cur = P;
+    for (int r = 2; r <= 16; r++) {  // [r] P; [16] P again as a check-free by-product (r = 16)
+        ge_add_cached(t, cur, cP);
+        ge_p1p1_to_p3(cur, t);
+        ge_p3_to_cached(c, cur);
+        row.store(r, c);
+    }
+    ge_p3 m16, m32, m64, s;
+    pts.load(1, m16);
+    pts.load(2, m32);
+    pts.load(3, m64);
+    ge_cached c16, c32, c64;
+    ge_p3_to_cached(c16, m16);
+    ge_p3_to_cached(c32, m32);
+    ge_p3_to_cached(c64, m64);
+    row.store(32, c32);
+    row.store(64, c64);
+    ge_add_cached(t, m32, c16);  // 48
+    ge_p1p1_to_p3(s, t);
+    ge_p3_to_cached(c, s);
+    row.store(48, c);
+    ge_add_cached(t, m64, c16);  // 80
+    ge_p1p1_to_p3(s, t);
+    ge_p3_to_cached(c, s);
+    row.store(80, c);
+    ge_add_cached(t, m64, c32);  // 96
+    ge_p1p1_to_p3(s, t);
+    ge_p3_to_cached(c, s);
+    row.store(96, c);
+    ge_add_cached(t, s, c16);    // 112
+    ge_p1p1_to_p3(s, t);
+    ge_p3_to_cached(c, s);
+    row.store(112, c);
+    ge_add_cached(t, m64, c64);  // 128
+    ge_p1p1_to_p3(s, t);
+    ge_p3_to_cached(c, s);
+    row.store(128, c);
+    fe invd;
+    fe_const(invd, PV_INVD);
+    uint32_t m[5];
+#pragma unroll
+    for (int w = 0; w < 5; w++) m[w] = need.word(w) & ~PV_SPARSE_PRE[w];
+    for (;;) {
+        int d = -1;
+#pragma unroll
+        for (int w = 4; w >= 0; w--)
+            if (m[w]) d = 32 * w + __builtin_ctz(m[w]);
+        if (d < 0) break;
+        m[d >> 5] &= ~(1u << (d & 31));
+        ge_cached cq, cr;
+        row.load(d & ~15, cq);
+        row.load(d & 15, cr);
+        ge_p3 q;  // 2 x T[16 q] in extended coordinates
+        fe_sub4p(q.X, cq.YplusX, cq.YminusX);
+        fe_carry(q.X, q.X);
+        fe_add(q.Y, cq.YplusX, cq.YminusX);
+        fe_carry(q.Y, q.Y);
+        fe_copy(q.Z, cq.Z2);
+        fe_mul(q.T, cq.T2d, invd);
+        ge_add_cached(t, q, cr);
+        ge_p1p1_to_p3(s, t);
+        ge_p3_to_cached(c, s);
+        row.store(d, c);
+    }
+}
+
 // ---------------------------------------------------------------- per-request accumulation
 // (Y+X, Y-X) of a table entry's first 20 words for a digit of sign `neg` (negation swaps them)
 PV_HD void pv_sel_pm(fe& ypx, fe& ymx, const uint32_t w[20], bool neg) {

@@ -25,6 +25,9 @@ static constexpr uint32_t PV_D[10] = {0x35978a3u, 0x0d37284u, 0x3156ebdu, 0x06a0
                                       0x179e898u, 0x3a03cbbu, 0x1ce7198u, 0x2e2b6ffu, 0x1480db3u};
 static constexpr uint32_t PV_D2[10] = {0x2b2f159u, 0x1a6e509u, 0x22add7au, 0x0d4141du, 0x0038052u,
                                        0x0f3d130u, 0x3407977u, 0x19ce331u, 0x1c56dffu, 0x0901b67u};
+// 1/d
+static constexpr uint32_t PV_INVD[10] = {0x1c9f843u, 0x03c9db3u, 0x285c4bcu, 0x0c213cau, 0x02d775au,
+                                         0x1b9cf66u, 0x3108a66u, 0x1c86562u, 0x1214d5cu, 0x10241fbu};
 // 1/2 = (p + 1) / 2
 static constexpr uint32_t PV_INV2[10] = {0x3fffff7u, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu,
                                          0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu, 0x0ffffffu};

@@ -61,6 +61,18 @@ static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tabl
 static constexpr uint64_t PV_KEYED_MIN = 4097;
 static constexpr uint32_t PV_ALLCOMB_KEYS = 2048;
 static constexpr uint32_t PV_ALLCOMB_CHUNK = 262144;
+// An all-comb chunk of at most PV_SPARSE_CHUNK requests and at most PV_SPARSE_PER_KEY requests per key
+// on average builds only the table entries its digits use (comb.h pv_comb_fill_sparse; the need
+// masks are set by pv_comb_prep_kernel). A/B on MI355X (1,024 signers, device time,
+// profiles/r02/ab_sparse_fill.txt): 6k requests 0.71 -> 0.54 ms, 10k 0.70 -> 0.56; at 32 requests
+// per key the per-position thread's serial additions outlast the parallel full fill (32k 0.69 ->
+// 0.72, 64k 0.74 -> 0.89), hence the per-key bound.
+#ifndef PV_SPARSE_CHUNK
+#define PV_SPARSE_CHUNK 65536
+#endif
+#ifndef PV_SPARSE_PER_KEY
+#define PV_SPARSE_PER_KEY 16
+#endif
 // Key chain launches per keyed chunk (the table fill of part p overlaps the chain of part p + 1).
 // A/B on MI355X (profiles/r02/ab_chain_parts.txt, interleaved): 1 part is best -- 10k requests
 // 0.70 ms device vs 0.74 (4 parts) / 0.92 (8), 1M 3.02 ms/step vs 3.04-3.11 / 3.15: the fill of a
@@ -228,6 +240,7 @@ struct Work {
 static constexpr int PV_SPLIT_KEYS = 0;        // distinct keys in the chunk
 static constexpr int PV_SPLIT_COMB_KEYS = 1;   // keys given a comb table
 static constexpr int PV_SPLIT_SLOTS = 2;       // requests (slots) of those keys
+static constexpr int PV_SPLIT_SPARSE = 3;      // 1: the comb tables are filled sparsely (small chunk)
 struct Gate {
     const uint32_t* split;
     const uint32_t* slot_req;
@@ -287,6 +300,7 @@ struct KeyWork {
     uint64_t* sverdict;
     uint32_t* key_cslot;   // [stride] node-side key cache slot of key id (PV_EMPTY: not cached)
     uint32_t* comb_cslot;  // [kcap] the same per comb index: its table is read from the cache
+    uint32_t* need;        // [PV_ALLCOMB_KEYS][32][5] needed |digit| bits per (comb index, position)
     const uint4* kc_tab;   // the cache's tables [cap][32][129][10] (keycache.h)
     uint32_t hmask;
     uint32_t kcap;
@@ -601,6 +615,8 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
     if (t == 0) {
         kw.nkeys[PV_SPLIT_COMB_KEYS] = min(ncand, kw.kcap);
         kw.nkeys[PV_SPLIT_SLOTS] = ctotal;
+        kw.nkeys[PV_SPLIT_SPARSE] =
+            all_comb && kw.chunk_n <= PV_SPARSE_CHUNK && kw.chunk_n <= PV_SPARSE_PER_KEY * nk ? 1u : 0u;
     }
 }
 
@@ -678,6 +694,18 @@ struct DevCombRow {
         ge_cached_store_words(w, c);
 #pragma unroll
         for (int q = 0; q < 10; q++) r[d * 10 + q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+    __device__ __forceinline__ void load(int d, ge_cached& c) const {
+        uint32_t w[40];
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            const uint4 v = r[d * 10 + q];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+        ge_cached_load_words(c, w);
     }
     __device__ __forceinline__ void load_half(int d, int h, uint32_t w[20]) const {
 #pragma unroll
@@ -955,7 +983,7 @@ __global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __re
 // nkeys * (hi - lo) * 8 items.
 __global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kernel(KeyWork kw, Gate gate, int lo,
                                                                                   int hi) {
-    if (!gate.keyed()) return;
+    if (!gate.keyed() || kw.nkeys[PV_SPLIT_SPARSE]) return;
     const uint32_t np = (uint32_t)(hi - lo);
     const uint32_t items = kw.nkeys[PV_SPLIT_COMB_KEYS] * np * PV_COMB_BLOCKS;
     for (uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x; it < items; it += gridDim.x * PV_BLOCK) {
@@ -966,6 +994,25 @@ __global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kerne
         const DevBasePts pts{DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10}, pos};
         pv_comb_fill_block(DevCombRow{kw.ctab + ((uint64_t)id * PV_COMB_POS + pos) * PV_COMB_ENT * 10}, pts, b);
     }
+}
+
+// Sparse variant for small chunks (PV_SPLIT_SPARSE): one thread per (comb key, position), only the
+// entries the chunk's digits use (pv_comb_fill_sparse). Runs on the main stream after
+// pv_comb_prep_kernel (need masks) and the key chain (bases). Sparse chunks have <= PV_ALLCOMB_KEYS
+// comb keys: the grid covers that many.
+struct DevNeed {
+    const uint32_t* p;
+    __device__ __forceinline__ uint32_t word(int w) const { return p[w]; }
+};
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_fill_sparse_kernel(KeyWork kw, Gate gate) {
+    if (!gate.keyed() || !kw.nkeys[PV_SPLIT_SPARSE]) return;
+    const uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x;
+    const uint32_t id = it / PV_COMB_POS;
+    const int pos = (int)(it % PV_COMB_POS);
+    if (id >= kw.nkeys[PV_SPLIT_COMB_KEYS] || kw.comb_cslot[id] != PV_EMPTY) return;
+    const DevBasePts pts{DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10}, pos};
+    pv_comb_fill_sparse(DevCombRow{kw.ctab + ((uint64_t)id * PV_COMB_POS + pos) * PV_COMB_ENT * 10}, pts,
+                        DevNeed{kw.need + ((uint64_t)id * PV_COMB_POS + pos) * 5});
 }
 
 // Key cache fill: comb index j of a put batch (tables built in the workspace by the chain / fill
@@ -1023,6 +1070,15 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
 #pragma unroll
     for (int j = 0; j < PV_BC2_POS; j++) ds.st(8 + j, i, (uint32_t)fb[j]);
     wk.flags[i] = ok ? 1u : 0u;
+    if (kw.nkeys[PV_SPLIT_SPARSE]) {  // small chunk: record which entries of each row this request uses
+        uint32_t* nd = kw.need + (uint64_t)kw.skey[i] * PV_COMB_POS * 5;
+#pragma unroll
+        for (int pos = 0; pos < PV_COMB_POS; pos++) {
+            const int e = pv_byte(ek[pos >> 2], pos);
+            const uint32_t d = (uint32_t)(e < 0 ? -e : e);
+            atomicOr(nd + pos * 5 + (d >> 5), 1u << (d & 31));
+        }
+    }
 }
 
 // Wide fixed-base comb rows (comb.h PV_BC2_*): row j = entries 0..PV_BC2_ENT-1 of [d 2^(W j)] B,
@@ -1485,6 +1541,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipMemsetAsync(kw.slot, 0xFF, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
             PV_HIP(hipMemsetAsync(kw.slot_cnt, 0, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
             PV_HIP(hipMemsetAsync(kw.nkeys, 0, 16, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipMemsetAsync(kw.need, 0, (uint64_t)PV_ALLCOMB_KEYS * PV_COMB_POS * 5 * 4, stream), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
@@ -1531,7 +1588,6 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                 hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, g_ctx.fstream, kw, gate, lo, hi);
                 PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             }
-            PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
         }
         if ((rc = mark(PV_STAGE_PREP))) return rc;
         if (keyed) {
@@ -1565,10 +1621,19 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             hipLaunchKernelGGL(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             // [S]B while the key stream finishes the tables, then join
             hipLaunchKernelGGL(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
                                gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            // a small chunk's sparse table fill (needs the chain's bases and the need masks comb_prep
+            // wrote) runs here on the main stream; for a large chunk it exits at once (the full
+            // fill runs on fstream) and its few gated blocks dispatch as comb_b retires
+            PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_chain[PV_CHAIN_MODE == 2 ? PV_CHAIN_PARTS - 1 : 0], 0),
+                   PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_key_fill_sparse_kernel, dim3(PV_ALLCOMB_KEYS * PV_COMB_POS / PV_BLOCK), dim3(PV_BLOCK),
+                               0, stream, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
@@ -1683,6 +1748,7 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.sverdict, S / 64 * 8), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_cslot, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.comb_cslot, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.need, (uint64_t)PV_ALLCOMB_KEYS * PV_COMB_POS * 5 * 4), PV_ERR_ALLOC);
         PV_HIP(hipMemset(kw.comb_cslot, 0xFF, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         std::vector<uint32_t> bc((size_t)PV_BCOMB_POS * PV_BCOMB_ENT * PV_BCOMB_STRIDE);
         {
@@ -1764,7 +1830,7 @@ void pv_shutdown(void) {
                     (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb, (void*)g_ctx.d_bc2, (void*)g_ctx.kw.key_count,
                     (void*)g_ctx.kw.key_cursor, (void*)g_ctx.kw.slot_req, (void*)g_ctx.kw.req_pos,
                     (void*)g_ctx.kw.skey, (void*)g_ctx.kw.sverdict, (void*)g_ctx.kw.key_cslot,
-                    (void*)g_ctx.kw.comb_cslot})
+                    (void*)g_ctx.kw.comb_cslot, (void*)g_ctx.kw.need})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : g_ctx.ev) (void)hipEventDestroy(e);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
@@ -2153,10 +2219,10 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
         f0 = f;
         const uint32_t m = (uint32_t)bslot.size();
         if (m == 0) continue;
-        const uint32_t cnt[3] = {m, m, 0};
+        const uint32_t cnt[4] = {m, m, 0, 0};  // keys, comb keys, slots, sparse = 0: every table in full
         PV_HIP(hipMemcpyAsync(k.d_put_pk, bpk.data(), bpk.size(), hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemcpyAsync(k.d_put_slot, bslot.data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-        PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, 12, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, 16, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemsetAsync(kw.comb_cslot, 0xFF, (uint64_t)m * 4, s), PV_ERR_LAUNCH);  // build every table
         const Gate gate{kw.nkeys, kw.slot_req};
         hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(m, PV_LP_CHAIN_BLOCKS)), dim3(64), 0, s,

@@ -108,6 +108,7 @@ struct HostBasePts {
 struct HostCombRow {
     uint32_t* r;  // [129][40]
     void store(int d, const ge_cached& c) const { ge_cached_store_words(r + 40 * d, c); }
+    void load(int d, ge_cached& c) const { ge_cached_load_words(c, r + 40 * d); }
     void load_half(int d, int h, uint32_t w[20]) const { memcpy(w, r + 40 * d + 20 * h, 80); }
 };
 struct HostCombRows {
@@ -280,6 +281,56 @@ int hc_sign_open_straus_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t*
     uint32_t enc[8];
     ge_p2_tobytes(enc, X, Y, Z);
     return ok && pv_words_equal(enc, in.R);
+}
+
+// pv_comb_fill_sparse (the small-chunk table fill) against pv_comb_fill_block (the full fill) for one
+// key: every position, a pseudo-random need set of about `density` x 129 entries (seeded); returns the
+// number of needed or always-built entries whose point differs from the full table's.
+struct HostNeed {
+    const uint32_t* p;
+    uint32_t word(int w) const { return p[w]; }
+};
+int hc_comb_fill_sparse_check(const uint8_t* pk, uint32_t seed, double density) {
+    uint32_t A[8];
+    memcpy(A, pk, 32);
+    ge_p3 negA;
+    if (!pv_key_ok_negate(negA, A)) return -1;
+    std::vector<ge_p3> bases(PV_COMB_POS * PV_COMB_PTS);
+    pv_comb_chain(HostBases{bases.data()}, negA);
+    std::vector<uint32_t> full((size_t)PV_COMB_POS * PV_COMB_ENT * 40), sparse(full.size(), 0);
+    int bad = 0;
+    uint64_t st = seed * 6364136223846793005ull + 1442695040888963407ull;
+    for (int pos = 0; pos < PV_COMB_POS; pos++) {
+        for (int b = 0; b < PV_COMB_BLOCKS; b++)
+            pv_comb_fill_block(HostCombRow{full.data() + (size_t)pos * PV_COMB_ENT * 40},
+                               HostBasePts{bases.data() + pos * PV_COMB_PTS}, b);
+        uint32_t need[5] = {0, 0, 0, 0, 0};
+        for (int d = 0; d < PV_COMB_ENT; d++) {
+            st = st * 6364136223846793005ull + 1442695040888963407ull;
+            if ((double)(st >> 11) / 9007199254740992.0 < density) need[d >> 5] |= 1u << (d & 31);
+        }
+        pv_comb_fill_sparse(HostCombRow{sparse.data() + (size_t)pos * PV_COMB_ENT * 40},
+                            HostBasePts{bases.data() + pos * PV_COMB_PTS}, HostNeed{need});
+        for (int d = 0; d < PV_COMB_ENT; d++) {
+            const bool built = ((need[d >> 5] | PV_SPARSE_PRE[d >> 5]) >> (d & 31)) & 1;
+            if (!built) continue;
+            ge_cached a, c;
+            ge_cached_load_words(a, full.data() + ((size_t)pos * PV_COMB_ENT + d) * 40);
+            ge_cached_load_words(c, sparse.data() + ((size_t)pos * PV_COMB_ENT + d) * 40);
+            const fe* fa[3] = {&a.YplusX, &a.YminusX, &a.T2d};
+            const fe* fc[3] = {&c.YplusX, &c.YminusX, &c.T2d};
+            for (int k = 0; k < 3; k++) {
+                fe x, y;
+                fe_mul(x, *fa[k], c.Z2);
+                fe_mul(y, *fc[k], a.Z2);
+                uint32_t u[8], v[8];
+                fe_tobytes32(u, x);
+                fe_tobytes32(v, y);
+                if (memcmp(u, v, sizeof u)) bad++;
+            }
+        }
+    }
+    return bad;
 }
 
 // k = SHA-512(R||A||M) mod L through pv_prepare (exposes the hashing + reduction)

@@ -299,3 +299,16 @@ def test_straus_wide_b_vs_libsodium(hc, sodium, oracle):
         for _ in range(3):
             sm, pk = g.make(cls)
             assert bool(hc.hc_sign_open_straus_wide16(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
+
+
+def test_comb_sparse_fill_matches_full_fill(hc, oracle):
+    """pv_comb_fill_sparse (small-chunk table fill: [r] P by steps, the [16 q] P from the chain's
+    multiples, every other needed entry as T[16 q] + T[r]) builds exactly the points of the full fill
+    for every needed entry, at sparse and dense need sets, for prime-order and mixed-order keys."""
+    from vectors import ORDER8
+    rng = random.Random(12)
+    keys = [oracle.scalarmult_base(rng.randrange(1, L).to_bytes(32, "little")) for _ in range(2)]
+    keys.append(oracle.point_add(keys[0], ORDER8))
+    for j, pk in enumerate(keys):
+        for density in (0.05, 0.3, 1.0):
+            assert hc.hc_comb_fill_sparse_check(pk, ctypes.c_uint32(j * 7 + 1), ctypes.c_double(density)) == 0, density
