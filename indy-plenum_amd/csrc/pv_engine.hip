@@ -810,11 +810,22 @@ struct DevBStage {  // fixed-base comb rows, entries of PV_BCOMB_STRIDE words (8
     }
 };
 
+// The key chain is the keyed path's long serial dependency and shares SIMDs with the per-request
+// prep kernel: its waves take issue priority (PV_CHAIN_PRIO, s_setprio).
+#ifndef PV_CHAIN_PRIO
+#define PV_CHAIN_PRIO 3
+#endif
+__device__ __forceinline__ void pv_chain_prio() {
+#if PV_CHAIN_PRIO > 0
+    __builtin_amdgcn_s_setprio(PV_CHAIN_PRIO);
+#endif
+}
+
 // Per distinct key: libsodium's key checks, -A, and the chain of bases [256^i](-A).
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
                                                                     Gate gate) {
     if (!gate.keyed()) return;
-    __builtin_amdgcn_s_setprio(3);
+    pv_chain_prio();
     const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;  // comb index
     if (id >= kw.nkeys[PV_SPLIT_COMB_KEYS] || kw.comb_cslot[id] != PV_EMPTY) return;
     uint32_t A[8];
@@ -893,7 +904,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const ui
     if (!gate.keyed()) return;
     // the chain is the batch's critical path and shares SIMDs with the per-request prep kernel:
     // take issue priority over it
-    __builtin_amdgcn_s_setprio(3);
+    pv_chain_prio();
     const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t nk = kw.nkeys[PV_SPLIT_COMB_KEYS];
     const uint32_t id = g >> 2;  // comb index
@@ -971,7 +982,7 @@ __global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __re
     if (!gate.keyed()) return;
     const uint32_t nk = kw.nkeys[PV_SPLIT_COMB_KEYS];
     if (blockIdx.x >= nk) return;
-    __builtin_amdgcn_s_setprio(3);
+    pv_chain_prio();
     const LpLane c = LpLane::make();
     const LpConsts K = LpConsts::make(c);
     for (uint32_t id = blockIdx.x; id < nk; id += gridDim.x)
