@@ -640,6 +640,11 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_unpermute_kernel(uint64_t n, KeyW
     if (r < n) {
         const uint32_t s = kw.req_pos[r];
         ok = (kw.sverdict[s >> 6] >> (s & 63)) & 1;
+        // leave the key hash table empty for the next keyed chunk (instead of a 16 MB memset there):
+        // every occupied slot is some request's slot
+        const uint32_t h = kw.req_key[r];
+        kw.slot[h] = PV_EMPTY;
+        kw.slot_cnt[h] = 0u;
     }
     const uint64_t bits = __ballot(ok);
     if ((threadIdx.x & 63) == 0 && r < n) verdict[r >> 6] = bits;
@@ -1012,7 +1017,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kerne
 // pv_comb_prep_kernel (need masks) and the key chain (bases). Sparse chunks have <= PV_ALLCOMB_KEYS
 // comb keys: the grid covers that many.
 struct DevNeed {
-    const uint32_t* p;
+    const uint32_t* p;  // the position's 5 mask words (registers of the caller)
     __device__ __forceinline__ uint32_t word(int w) const { return p[w]; }
 };
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_fill_sparse_kernel(KeyWork kw, Gate gate) {
@@ -1020,10 +1025,18 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_fill_sparse_kernel(KeyWork kw
     const uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t id = it / PV_COMB_POS;
     const int pos = (int)(it % PV_COMB_POS);
-    if (id >= kw.nkeys[PV_SPLIT_COMB_KEYS] || kw.comb_cslot[id] != PV_EMPTY) return;
+    if (id >= kw.nkeys[PV_SPLIT_COMB_KEYS]) return;
+    uint32_t* nd = kw.need + ((uint64_t)id * PV_COMB_POS + pos) * 5;
+    uint32_t m[5];
+#pragma unroll
+    for (int w = 0; w < 5; w++) {  // read and clear: the masks start empty for the next sparse chunk
+        m[w] = nd[w];
+        nd[w] = 0u;
+    }
+    if (kw.comb_cslot[id] != PV_EMPTY) return;
     const DevBasePts pts{DevBases{kw.bases + (uint64_t)id * PV_COMB_POS * PV_COMB_PTS * 10}, pos};
     pv_comb_fill_sparse(DevCombRow{kw.ctab + ((uint64_t)id * PV_COMB_POS + pos) * PV_COMB_ENT * 10}, pts,
-                        DevNeed{kw.need + ((uint64_t)id * PV_COMB_POS + pos) * 5});
+                        DevNeed{m});
 }
 
 // Key cache fill: comb index j of a put batch (tables built in the workspace by the chain / fill
@@ -1349,6 +1362,7 @@ struct Ctx {
     hipEvent_t ev_tables_ready = nullptr;    // comb tables done (fstream -> main)
     hipStream_t fstream = nullptr;           // table fill, one launch per chain part
     hipEvent_t ev_chain[PV_CHAIN_PARTS] = {};  // chain part done (kstream -> fstream)
+    hipEvent_t ev_prep_done = nullptr;        // comb_prep done: need masks ready (main -> fstream)
     hipStream_t sstream = nullptr;           // Straus-path slots of a split chunk, overlapped
     hipEvent_t ev_straus_done = nullptr;     // their q / flags written (sstream -> main)
     // Workspace hand-over between callers' streams: every launch ends by recording ev_launch_done
@@ -1360,6 +1374,7 @@ struct Ctx {
     Work work{nullptr, nullptr, nullptr, nullptr, 0};
     KeyWork kw{};
     bool last_keyed = false;  // the most recent chunk ran the dedup / split kernels
+    bool slots_dirty = true;  // the key hash table / need masks may hold entries (cleared before use)
     bool last_latency = false;  // the most recent launch took the latency path
     bool verdict_zeroed = false;  // the caller's verdict words are already 0 (pv_verify_batch)
     uint32_t last_split[3] = {0, 0, 0};  // PV_SPLIT_* of it, read back by pv_last_path
@@ -1549,10 +1564,16 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         kw.kc_tab = g_ctx.kc.d_tab;
         const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
         if (keyed) {
-            PV_HIP(hipMemsetAsync(kw.slot, 0xFF, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
-            PV_HIP(hipMemsetAsync(kw.slot_cnt, 0, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
+            // the hash table and need masks are left empty by the previous keyed chunk (unpermute and
+            // sparse fill kernels); after an enqueue failure they may not be, and are cleared here
+            if (g_ctx.slots_dirty) {
+                PV_HIP(hipMemsetAsync(kw.slot, 0xFF, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
+                PV_HIP(hipMemsetAsync(kw.slot_cnt, 0, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
+                PV_HIP(hipMemsetAsync(kw.need, 0, (uint64_t)PV_ALLCOMB_KEYS * PV_COMB_POS * 5 * 4, stream),
+                       PV_ERR_LAUNCH);
+            }
+            g_ctx.slots_dirty = true;  // until this chunk's unpermute kernel is enqueued
             PV_HIP(hipMemsetAsync(kw.nkeys, 0, 16, stream), PV_ERR_LAUNCH);
-            PV_HIP(hipMemsetAsync(kw.need, 0, (uint64_t)PV_ALLCOMB_KEYS * PV_COMB_POS * 5 * 4, stream), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
@@ -1632,19 +1653,18 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             hipLaunchKernelGGL(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            // a small chunk's sparse table fill (needs the chain's bases and the need masks comb_prep
+            // writes) runs on fstream after the full fill; for a large chunk it exits at once
+            PV_HIP(hipEventRecord(g_ctx.ev_prep_done, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipStreamWaitEvent(g_ctx.fstream, g_ctx.ev_prep_done, 0), PV_ERR_LAUNCH);
+            hipLaunchKernelGGL(pv_key_fill_sparse_kernel, dim3(PV_ALLCOMB_KEYS * PV_COMB_POS / PV_BLOCK), dim3(PV_BLOCK),
+                               0, g_ctx.fstream, kw, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             // [S]B while the key stream finishes the tables, then join
             hipLaunchKernelGGL(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
                                gate);
-            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            // a small chunk's sparse table fill (needs the chain's bases and the need masks comb_prep
-            // wrote) runs here on the main stream; for a large chunk it exits at once (the full
-            // fill runs on fstream) and its few gated blocks dispatch as comb_b retires
-            PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_chain[PV_CHAIN_MODE == 2 ? PV_CHAIN_PARTS - 1 : 0], 0),
-                   PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_key_fill_sparse_kernel, dim3(PV_ALLCOMB_KEYS * PV_COMB_POS / PV_BLOCK), dim3(PV_BLOCK),
-                               0, stream, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
@@ -1677,6 +1697,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             hipLaunchKernelGGL(pv_unpermute_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw,
                                d_verdict + c0 / 64, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            g_ctx.slots_dirty = false;
         }
         if ((rc = mark(PV_NSTAGES))) return rc;
     }
@@ -1720,6 +1741,7 @@ int pv_init(int device) {
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.fstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     for (auto& e : g_ctx.ev_chain) PV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_prep_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
@@ -1851,6 +1873,7 @@ void pv_shutdown(void) {
     if (g_ctx.fstream) (void)hipStreamDestroy(g_ctx.fstream);
     for (hipEvent_t e : g_ctx.ev_chain)
         if (e) (void)hipEventDestroy(e);
+    if (g_ctx.ev_prep_done) (void)hipEventDestroy(g_ctx.ev_prep_done);
     if (g_ctx.sstream) (void)hipStreamDestroy(g_ctx.sstream);
     if (g_ctx.ev_straus_done) (void)hipEventDestroy(g_ctx.ev_straus_done);
     if (g_ctx.ev_launch_done) (void)hipEventDestroy(g_ctx.ev_launch_done);
