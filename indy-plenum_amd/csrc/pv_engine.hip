@@ -84,6 +84,23 @@ static_assert(32 % PV_CHAIN_PARTS == 0, "PV_CHAIN_PARTS must divide the 32 comb 
 #ifndef PV_LP_CHAIN_BLOCKS
 #define PV_LP_CHAIN_BLOCKS 2048  // waves of the limb-parallel key chain (one key each at a time)
 #endif
+// Dedup contention (1,024 signers x ~1,000 requests each per 1M chunk). Kernel times on MI355X
+// (rocprofv3, profiles/r02/ab_dedup_seed.txt): insert + assign 143 us with one atomic counter per
+// key and an atomic first read; 95 us with the seed pre-pass; 92 with a plain first read; 85 us
+// (+ 8 us seed) with the counters split 8 ways (16: 86, 32: 87 -- the assign kernel's sums grow).
+#ifndef PV_KEY_SEED
+#define PV_KEY_SEED 4096  // requests of a keyed chunk whose keys are inserted first (pv_key_seed_kernel)
+#endif
+#ifndef PV_INSERT_PLAIN_LOAD
+#define PV_INSERT_PLAIN_LOAD 1  // the insert's first slot read is a plain load (0: an atomic load)
+#endif
+// Per-key request counters of the dedup are split PV_RANK_SUB ways (sub-table = the request's
+// workgroup index mod PV_RANK_SUB), so the ~1,000 requests of a hot key queue on PV_RANK_SUB
+// device-scope atomics instead of one; the assign kernel turns the sub-counts into offsets.
+#ifndef PV_RANK_SUB
+#define PV_RANK_SUB 8
+#endif
+static_assert((PV_RANK_SUB & (PV_RANK_SUB - 1)) == 0, "PV_RANK_SUB must be a power of two");
 #ifndef PV_LATENCY_MAX
 #define PV_LATENCY_MAX 4096  // AUTO: batches up to this size take the latency path (pv_latency.hip)
 #endif
@@ -258,8 +275,10 @@ struct Gate {
 // Keyed workspace (comb.h). The hash table maps a 32-byte key to the index of the first request
 // that carried it; slot_id gives the dense key id of an owned slot (ids < chunk size).
 //   slot     [H] u32   owner request index, PV_EMPTY = free
-//   slot_id  [H] u32   dense key id of an owned slot;  slot_cnt [H] requests carrying its key
-//   req_key  [stride]  the request's hash slot;         req_rank [stride] its rank among them
+//   slot_id  [H] u32   dense key id of an owned slot
+//   slot_cnt [PV_RANK_SUB][H]  requests carrying the key per sub-table (request workgroup mod
+//            PV_RANK_SUB); the assign kernel replaces each nonzero count by its offset in the key
+//   req_key  [stride]  the request's hash slot;         req_rank [stride] its rank in its sub-table
 //   nkeys    [3]       PV_SPLIT_* counters (see Gate)
 //   key_owner[stride]  a request carrying key id
 //   key_cid  [stride]  comb index of key id (PV_EMPTY: its requests take the Straus path)
@@ -492,6 +511,10 @@ __device__ __forceinline__ uint32_t pv_key_hash(const uint32_t A[8], uint32_t se
     return h;
 }
 
+// Sub-table of request i's per-key counter: its workgroup of the insert / scatter / unpermute grids
+// (all PV_BLOCK requests per workgroup, request i in workgroup i / PV_BLOCK).
+__device__ __forceinline__ uint32_t pv_rank_sub(uint32_t i) { return (i / PV_BLOCK) & (PV_RANK_SUB - 1u); }
+
 // Dedup 1/2: open-addressing insert of every request's key; req_key[i] = the key's slot.
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* __restrict__ pk, uint64_t n,
                                                                   KeyWork kw) {
@@ -503,7 +526,13 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* 
     for (uint32_t probe = 0; probe <= kw.hmask; probe++) {  // the table is >= 2x the chunk: never full
         // a plain read first: once a key is in, its other requests find it without an atomic (the
         // atomics of one key's requests all queue on one slot)
+#if PV_INSERT_PLAIN_LOAD
+        // a plain (L2-cached) read: a stale PV_EMPTY only sends the request to the CAS, which returns
+        // the slot's current value; a slot never changes once set within the kernel
+        uint32_t cur = kw.slot[h];
+#else
         uint32_t cur = __hip_atomic_load(&kw.slot[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         if (cur == PV_EMPTY) cur = atomicCAS(&kw.slot[h], PV_EMPTY, i);
         if (cur == PV_EMPTY) break;
         uint32_t B[8];
@@ -514,7 +543,28 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* 
     kw.req_key[i] = h;
     // the request's rank among its key's requests, and (final after this kernel) the key's count;
     // the 1,024-odd counters of a batch sit on distinct hash slots, i.e. mostly distinct L2 lines
-    kw.req_rank[i] = atomicAdd(&kw.slot_cnt[h], 1u);
+    kw.req_rank[i] = atomicAdd(&kw.slot_cnt[pv_rank_sub(i) * (kw.hmask + 1ull) + h], 1u);
+}
+
+// Dedup 0/2: the first requests of the chunk claim their keys' slots before the full insert, so a
+// frequent key is already in the table when its other requests arrive: the full insert then finds
+// it with a plain read instead of hundreds of its requests racing a compare-and-swap on one slot.
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_seed_kernel(const uint8_t* __restrict__ pk, uint64_t n,
+                                                                KeyWork kw) {
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t A[8];
+    pv_load_pk(A, pk, i);
+    uint32_t h = pv_key_hash(A, kw.seed) & kw.hmask;
+    for (uint32_t probe = 0; probe <= kw.hmask; probe++) {
+        uint32_t cur = __hip_atomic_load(&kw.slot[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == PV_EMPTY) cur = atomicCAS(&kw.slot[h], PV_EMPTY, i);
+        if (cur == PV_EMPTY) return;
+        uint32_t B[8];
+        pv_load_pk(B, pk, cur);
+        if (pv_words_equal(A, B)) return;
+        h = (h + 1) & kw.hmask;
+    }
 }
 
 // Dedup 2/2: the owner request of each occupied slot takes a dense key id (one atomic per wave)
@@ -534,7 +584,18 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, Key
     const uint32_t id = base + (uint32_t)__popcll(owners & ((1ull << lane) - 1ull));  // < n
     kw.slot_id[s] = id;
     kw.key_owner[id] = i;
-    kw.key_count[id] = kw.slot_cnt[s];
+    // sub-counts -> offsets (zero counts stay zero: no request reads them); all loads before the stores
+    uint32_t v[PV_RANK_SUB];
+    const uint64_t H = kw.hmask + 1ull;
+#pragma unroll
+    for (int u = 0; u < PV_RANK_SUB; u++) v[u] = kw.slot_cnt[u * H + s];
+    uint32_t total = 0;
+#pragma unroll
+    for (int u = 0; u < PV_RANK_SUB; u++) {
+        if (v[u]) kw.slot_cnt[u * H + s] = total;
+        total += v[u];
+    }
+    kw.key_count[id] = total;
 }
 
 // Dedup 2b (only when the node-side key cache holds keys): every distinct key id looks its key up
@@ -624,8 +685,10 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_scatter_kernel(uint64_t n, KeyWork kw) {
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
     if (i >= n) return;
-    const uint32_t id = kw.slot_id[kw.req_key[i]];
-    const uint32_t pos = kw.key_cursor[id] + kw.req_rank[i];
+    const uint32_t h = kw.req_key[i];
+    const uint32_t id = kw.slot_id[h];
+    const uint32_t sub_off = kw.slot_cnt[pv_rank_sub(i) * (kw.hmask + 1ull) + h];
+    const uint32_t pos = kw.key_cursor[id] + sub_off + kw.req_rank[i];
     kw.slot_req[pos] = i;
     kw.req_pos[i] = pos;
     kw.skey[pos] = kw.key_cid[id];
@@ -644,7 +707,7 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_unpermute_kernel(uint64_t n, KeyW
         // every occupied slot is some request's slot
         const uint32_t h = kw.req_key[r];
         kw.slot[h] = PV_EMPTY;
-        kw.slot_cnt[h] = 0u;
+        kw.slot_cnt[pv_rank_sub(r) * (kw.hmask + 1ull) + h] = 0u;
     }
     const uint64_t bits = __ballot(ok);
     if ((threadIdx.x & 63) == 0 && r < n) verdict[r >> 6] = bits;
@@ -1568,12 +1631,19 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             // sparse fill kernels); after an enqueue failure they may not be, and are cleared here
             if (g_ctx.slots_dirty) {
                 PV_HIP(hipMemsetAsync(kw.slot, 0xFF, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
-                PV_HIP(hipMemsetAsync(kw.slot_cnt, 0, (uint64_t)(kw.hmask + 1) * 4, stream), PV_ERR_LAUNCH);
+                PV_HIP(hipMemsetAsync(kw.slot_cnt, 0, (uint64_t)(kw.hmask + 1) * 4 * PV_RANK_SUB, stream),
+                       PV_ERR_LAUNCH);
                 PV_HIP(hipMemsetAsync(kw.need, 0, (uint64_t)PV_ALLCOMB_KEYS * PV_COMB_POS * 5 * 4, stream),
                        PV_ERR_LAUNCH);
             }
             g_ctx.slots_dirty = true;  // until this chunk's unpermute kernel is enqueued
             PV_HIP(hipMemsetAsync(kw.nkeys, 0, 16, stream), PV_ERR_LAUNCH);
+            if (PV_KEY_SEED > 0 && m > 16ull * PV_KEY_SEED) {  // small chunks: no contention worth a launch
+                const uint64_t ms = std::min<uint64_t>(m, PV_KEY_SEED);
+                hipLaunchKernelGGL(pv_key_seed_kernel, dim3((unsigned)((ms + PV_BLOCK - 1) / PV_BLOCK)), dim3(PV_BLOCK), 0,
+                                   stream, d_pk + 32 * c0, ms, kw);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            }
             hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
@@ -1763,7 +1833,7 @@ int pv_init(int device) {
         kw.seed = (uint32_t)std::random_device{}() | 1u;
         PV_HIP(hipMalloc((void**)&kw.slot, H * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.slot_id, H * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.slot_cnt, H * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.slot_cnt, H * 4 * PV_RANK_SUB), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_key, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_rank, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.nkeys, 256), PV_ERR_ALLOC);
