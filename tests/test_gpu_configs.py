@@ -290,3 +290,35 @@ def test_medium_chunks_all_comb_or_split(native, sodium):
             got = native.verify_sm_batch(blob, off, pks)
             native.set_path(native.PV_PATH_AUTO)
             assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
+
+
+def test_dedup_hot_keys(native):
+    """Key skew far beyond the bench's ~1,000 requests per signer, in a chunk large enough for the
+    dedup's seed pass (> 65,536 requests): 120k requests of one signer, 60k of another and 20k
+    spread over the 1,024-signer pool, shuffled, ~0.1 % corrupted. Every key's requests must land in
+    one contiguous slot range (the per-key counters are split 8 ways and re-joined by the assign
+    kernel), so AUTO (all keys comb here) and forced COMB must equal libsodium bit for bit."""
+    import nym_workload
+    from oracle.oracle import cpu_verdicts
+    blob, off, pks = nym_workload.generate(0, 4096)
+    rng = np.random.default_rng(21)
+    src = np.concatenate([np.zeros(120000, np.int64), np.ones(60000, np.int64),
+                          rng.integers(2, 4096, 20000)])
+    src = src[rng.permutation(len(src))]
+    lens = (off[1:] - off[:-1]).astype(np.int64)[src]
+    off2 = np.zeros(len(src) + 1, np.uint64)
+    np.cumsum(lens, out=off2[1:])
+    blob2 = np.concatenate([blob[int(off[s]):int(off[s + 1])] for s in src])
+    pks2 = np.ascontiguousarray(pks[src])
+    n = len(src)
+    for i in rng.choice(n, 200, replace=False):
+        blob2[int(off2[i]) + int(rng.integers(0, 64))] ^= 1 << int(rng.integers(0, 8))
+    want = cpu_verdicts(blob2, off2, pks2)
+    assert 150 < (~want).sum() <= 200
+    for path in (native.PV_PATH_AUTO, native.PV_PATH_COMB):
+        native.set_path(path)
+        got = native.verify_sm_batch(blob2, off2, pks2)
+        split = native.last_split()
+        native.set_path(native.PV_PATH_AUTO)
+        assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
+        assert split == (1024, 1024, n), (path, split)
