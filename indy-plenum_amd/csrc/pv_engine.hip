@@ -1440,6 +1440,7 @@ struct Ctx {
     bool slots_dirty = true;  // the key hash table / need masks may hold entries (cleared before use)
     bool last_latency = false;  // the most recent launch took the latency path
     bool verdict_zeroed = false;  // the caller's verdict words are already 0 (pv_verify_batch)
+    bool keyed_hint = false;      // pv_verify_batch saw few distinct keys: keyed path below PV_LATENCY_MAX
     uint32_t last_split[3] = {0, 0, 0};  // PV_SPLIT_* of it, read back by pv_last_path
     uint4* d_bcomb = nullptr;  // fixed-base comb T_B (radix 65536; latency path)
     uint4* d_bc2 = nullptr;    // wide fixed-base comb T_B2 (radix 2^W; comb path's [S]B)
@@ -1576,7 +1577,8 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
     const int nchunks = (int)((n + cap - 1) / cap);
     constexpr int NE = PV_NSTAGES + 1;
     // small batches: one wave pair per request (pv_latency.hip); forced LATENCY takes it at any size
-    const bool latency = g_ctx.path == PV_PATH_LATENCY || (g_ctx.path == PV_PATH_AUTO && n <= PV_LATENCY_MAX);
+    const bool latency = g_ctx.path == PV_PATH_LATENCY ||
+                         (g_ctx.path == PV_PATH_AUTO && n <= PV_LATENCY_MAX && !g_ctx.keyed_hint);
     g_ctx.last_latency = latency;
     int evb = 0;
     if (g_ctx.timing) {
@@ -1617,7 +1619,8 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         // its comb table already built: its requests take the comb path at any count.
         const PvKeyCacheView kcv = kc_view();
         const bool kc_active = kcv.hmask != 0;
-        const bool keyed = g_ctx.path == PV_PATH_COMB || (g_ctx.path == PV_PATH_AUTO && m >= PV_KEYED_MIN);
+        const bool keyed = g_ctx.path == PV_PATH_COMB ||
+                           (g_ctx.path == PV_PATH_AUTO && (m >= PV_KEYED_MIN || g_ctx.keyed_hint));
         Gate gate{nullptr, nullptr};
         g_ctx.last_keyed = keyed;
         KeyWork kw = g_ctx.kw;
@@ -2120,6 +2123,42 @@ static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* s
     return err.load() ? fail(PV_ERR_LAUNCH, "hipMemcpyAsync (request blob) failed") : PV_OK;
 }
 
+// AUTO between the latency path and the keyed path for a host batch of PV_KEYED_HINT_MIN..
+// PV_LATENCY_MAX requests: the device cannot count keys before the path is chosen, the host can
+// (~10 us for 4,096 keys). With >= 3 requests per key on average (and at most PV_ALLCOMB_KEYS keys:
+// every key a comb key, sparse fill) the keyed path is faster -- MI355X, 1,024 signers, PCIe
+// included (profiles/r02/latency_vs_keyed_crossover.txt): 3,072 requests 0.64 vs 0.71 ms, 4,096
+// 0.65 vs 0.92; at 2 requests per key (2,048) the latency path still wins (0.58 vs 0.61). Keys in
+// the node-side key cache make the latency path faster still: no hint while the cache holds keys.
+#ifndef PV_KEYED_HINT_MIN
+#define PV_KEYED_HINT_MIN 2049
+#endif
+static bool pv_keyed_hint(const uint8_t* pk, uint64_t n) {
+    if (g_ctx.path != PV_PATH_AUTO || n < PV_KEYED_HINT_MIN || n > PV_LATENCY_MAX) return false;
+    if (g_ctx.kc.enabled && !g_ctx.kc.index.empty()) return false;
+    // distinct keys by open addressing on the keys' first 16 bytes (a heuristic: a rare collision
+    // only miscounts, the verdicts do not depend on the path)
+    constexpr uint32_t H = 16384;  // > 2 x PV_LATENCY_MAX
+    static_assert(H >= 2 * PV_LATENCY_MAX, "hint table too small");
+    static thread_local std::vector<uint64_t> tab;
+    tab.assign(2 * H, 0);
+    uint64_t distinct = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t a, b;
+        memcpy(&a, pk + 32 * i, 8);
+        memcpy(&b, pk + 32 * i + 8, 8);
+        a |= 1;  // (0, 0) marks an empty entry
+        uint32_t h = (uint32_t)((a * 0x9E3779B97F4A7C15ull) >> 50) & (H - 1);
+        while (tab[2 * h] && !(tab[2 * h] == a && tab[2 * h + 1] == b)) h = (h + 1) & (H - 1);
+        if (!tab[2 * h]) {
+            tab[2 * h] = a;
+            tab[2 * h + 1] = b;
+            distinct++;
+        }
+    }
+    return distinct <= PV_ALLCOMB_KEYS && 3 * distinct <= n;
+}
+
 int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
                     uint8_t* verdict_bits) {
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_verify_batch: call pv_init first");
@@ -2176,8 +2215,10 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     }
     uint64_t* dver = reinterpret_cast<uint64_t*>(d + pk_bytes + off_bytes);
     g_ctx.verdict_zeroed = true;
+    g_ctx.keyed_hint = pv_keyed_hint(pk, n);
     rc = launch(d + pk_bytes + off_bytes + v_bytes, reinterpret_cast<const uint64_t*>(d + pk_bytes), n, d, dver, s);
     g_ctx.verdict_zeroed = false;
+    g_ctx.keyed_hint = false;
     if (rc) return rc;
     uint64_t* hver = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
     PV_HIP(hipMemcpyAsync(hver, dver, vwords * 8, hipMemcpyDeviceToHost, s), PV_ERR_LAUNCH);

@@ -322,3 +322,24 @@ def test_dedup_hot_keys(native):
         native.set_path(native.PV_PATH_AUTO)
         assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
         assert split == (1024, 1024, n), (path, split)
+
+
+def test_medium_host_batch_path_hint(native, sodium):
+    """Host batches between 2,048 and 4,096 requests: with >= 3 requests per key AUTO takes the keyed
+    path (the host counts the keys, pv_keyed_hint), with one-off keys the latency path; both
+    bit-exact against libsodium, as are the forced paths."""
+    from oracle.oracle import cpu_verdicts
+    for n_signed, n_single, want_path in ((4096, 0, native.PV_PATH_COMB), (3072, 0, native.PV_PATH_COMB),
+                                          (2048, 0, native.PV_PATH_LATENCY),
+                                          (0, 3000, native.PV_PATH_LATENCY)):
+        blob, off, pks = _split_batch(sodium, n_signed, n_single, seed=31 + n_signed)
+        want = cpu_verdicts(blob, off, pks)
+        got = native.verify_sm_batch(blob, off, pks)
+        path, _ = native.last_path()
+        assert path == want_path, (n_signed, n_single, path)
+        assert np.array_equal(got, want), (n_signed, n_single, np.nonzero(got != want)[0][:10])
+        for forced in (native.PV_PATH_LATENCY, native.PV_PATH_COMB):
+            native.set_path(forced)
+            got = native.verify_sm_batch(blob, off, pks)
+            native.set_path(native.PV_PATH_AUTO)
+            assert np.array_equal(got, want), (forced, np.nonzero(got != want)[0][:10])
