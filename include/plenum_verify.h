@@ -107,12 +107,14 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
  *                   one chain, [S]B from the fixed-base comb, [k](-A) by 252 doublings + 64
  *                   additions, and the comparison with R without an inversion. One kernel launch;
  *                   the fastest path for small batches (Plenum's 100 / 1,000-message quotas)
- *   PV_PATH_AUTO    (default) batches of <= 4,096 requests take the latency path; otherwise
- *                   per chunk of >= 32,768 requests: deduplicate keys, give a comb table
- *                   to every key with >= 48 requests in the chunk (a table costs about what ~50
- *                   requests save) and verify the other requests on the Straus path in the same
- *                   launch; smaller chunks go Straus. Split on the device, so
- *                   pv_verify_batch_device stays asynchronous.
+ *   PV_PATH_AUTO    (default) batches of <= 4,096 requests take the latency path, except host
+ *                   batches (pv_verify_batch) of 2,049-4,096 requests with >= 3 requests per key
+ *                   (counted on the host), which go keyed; otherwise per chunk: deduplicate keys,
+ *                   give a comb table to every key with >= 48 requests in the chunk (a table costs
+ *                   about what ~50 requests save) -- to every key when the chunk has <= 2,048 keys
+ *                   and <= 256k requests -- and verify the other requests on the Straus path in
+ *                   the same launch; a tail chunk of <= 4,096 requests goes Straus. Split on the
+ *                   device, so pv_verify_batch_device stays asynchronous.
  * Every path returns bit-identical verdicts. */
 #define PV_PATH_AUTO 0
 #define PV_PATH_STRAUS 1
