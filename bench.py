@@ -364,16 +364,17 @@ CONFIG5_TOTAL = 1 << 26  # configs[4]: 64M requests over the node's GPUs
 
 class Comm:
     """Multi-GPU harness without a framework: the RCCL communicator of libplenum_verify is the only
-    channel. Rank 0's ncclUniqueId reaches the other ranks through a file named after the launcher's
-    PID (torch.distributed.run starts every rank of one job from the same agent process, so the name
-    is unique per job and never stale); barrier = a one-word all-gather + device sync; the max over
+    channel. Rank 0's ncclUniqueId reaches the other ranks through a file named after the job
+    (PV_BENCH_JOB from bench.py's own launcher, else the launcher's PID and port:
+    torch.distributed.run starts every rank of one job from the same agent process, so the name is
+    unique per job and never stale); barrier = a one-word all-gather + device sync; the max over
     ranks of a host time = an all-gather of every rank's time."""
 
     def __init__(self, world, rank, L):
         import tempfile
         self.world, self.rank, self.L = world, rank, L
-        path = os.path.join(tempfile.gettempdir(), "pv_bench_%d_%s.uid" % (
-            os.getppid(), os.environ.get("MASTER_PORT", "0")))
+        job = os.environ.get("PV_BENCH_JOB") or "%d_%s" % (os.getppid(), os.environ.get("MASTER_PORT", "0"))
+        path = os.path.join(tempfile.gettempdir(), "pv_bench_%s.uid" % job)
         uid = (ctypes.c_uint8 * 128)()
         if rank == 0:
             _native.check(L.pv_comm_unique_id(uid), "pv_comm_unique_id")
@@ -461,6 +462,75 @@ def config3_leg(db_like, blob0, off, pks, steps, timed_fn):
     return res, got, (blob3, off, pks3)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, cmd, poll_s=0.2):
+    """Start n fresh rank processes of `cmd` (one per GPU), each with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT / PV_BENCH_JOB in its environment, relay rank 0's stdout
+    and return 0 only if every rank exits 0. When a rank fails, the others (which would wait in a
+    collective forever) are terminated by their exact PIDs. The caller never touches the GPU:
+    this runs before the library is loaded (plain subprocess, never exec)."""
+    import subprocess
+    port = _free_port()
+    job = "%d_%d" % (os.getpid(), port)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PV_BENCH_JOB=job)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else subprocess.DEVNULL))
+    t0 = time.time()
+    rc = 0
+    live = list(range(n))
+    last_note = t0
+    while live:
+        time.sleep(poll_s)
+        for r in list(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.remove(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log("launcher: rank %d exited with %d after %.1f s; stopping the other ranks" % (r, code, time.time() - t0))
+                for o in live:
+                    procs[o].terminate()
+        if rc and live:
+            deadline = time.time() + 30
+            while live and time.time() < deadline:
+                live = [o for o in live if procs[o].poll() is None]
+                time.sleep(poll_s)
+            for o in live:
+                procs[o].kill()
+                procs[o].wait()
+            live = []
+        if live and time.time() - last_note > 60:
+            last_note = time.time()
+            log("launcher: %d of %d ranks still running (%.0f s)" % (len(live), n, time.time() - t0))
+    return rc
+
+
+def _rank_stub():
+    """--rank-stub: what a rank saw (tests of the launcher; never touches the GPU)."""
+    keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "PV_BENCH_JOB")
+    out = os.environ.get("PV_BENCH_STUB_DIR")
+    rec = {k: os.environ.get(k) for k in keys}
+    rec["RANK"] = rec["RANK"] or "0"
+    if out:
+        with open(os.path.join(out, "rank%s.json" % rec["RANK"]), "w") as f:
+            json.dump(rec, f)
+    if os.environ.get("PV_BENCH_STUB_FAIL_RANK") == rec["RANK"]:
+        sys.exit(3)
+    if rec["RANK"] == "0":
+        print(json.dumps({"stub": True, "world": int(rec["WORLD_SIZE"] or 1)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -479,7 +549,28 @@ def main():
     ap.add_argument("--dataset", default=None, help="npz from tools/nym_workload.py (profiling runs: no fork)")
     ap.add_argument("--no-ingress", action="store_true", help="skip the ingress / host-serialization measurements")
     ap.add_argument("--no-multisig", action="store_true", help="skip the configs[3] multi-signature measurement")
+    ap.add_argument("--rank-stub", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    # one process per GPU: under a launcher (torch.distributed.run) WORLD_SIZE must equal --gpus;
+    # without one, --gpus N > 1 starts the N ranks itself (fresh processes, before anything here
+    # has loaded the library or touched a GPU) and relays rank 0's line
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        log("bench.py: WORLD_SIZE=%s but --gpus %d: refusing to report a line for the wrong GPU count"
+            % (env_world, args.gpus))
+        sys.exit(2)
+    if env_world is None and args.gpus > 1:
+        t0 = time.perf_counter()
+        rc = spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+        log("launcher: %d ranks finished with rc %d in %.1f s" % (args.gpus, rc, time.perf_counter() - t0))
+        sys.exit(rc)
+    if args.gpus < 1:
+        log("bench.py: --gpus must be >= 1")
+        sys.exit(2)
+    if args.rank_stub:
+        _rank_stub()
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -524,11 +615,16 @@ def main():
 
     # the GPU runtime comes up only after the forked signing workers of the workload generator are
     # done: nothing forks once the device is initialised
+    t0 = time.perf_counter()
     _native.ensure_device(local_rank)
     L = _native.lib()
+    log("rank %d: device %d up (pv_init) in %.1f s" % (rank, local_rank, time.perf_counter() - t0))
+    t0 = time.perf_counter()
     db = DeviceBatch(blob, off, pks)
     comm = Comm(world, rank, L) if world > 1 else None
     d_all = db._alloc(db.words * 8 * world) if world > 1 else None
+    log("rank %d: batch uploaded%s in %.1f s" % (rank, " and communicator up" if comm else "",
+                                                 time.perf_counter() - t0))
 
     def step():
         db.verify()
@@ -564,10 +660,16 @@ def main():
 
     # headline: the default (AUTO) path selection
     _native.set_path(_native.PV_PATH_AUTO)
+    t0 = time.perf_counter()
     for _ in range(args.warmup):
         step()
+    _native.check(L.pv_sync(), "pv_sync")
+    log("rank %d: %d warm-up steps in %.1f s" % (rank, args.warmup, time.perf_counter() - t0))
+    t0 = time.perf_counter()
     elapsed, _ = timed(args.steps, stages=False)  # the headline: no stage events in the measured loop
     _, stage_ms = timed(args.steps)                # stage breakdown and the roofline kernel's launch time
+    log("rank %d: timed runs in %.1f s (headline %.3f s for %d steps)" % (rank, time.perf_counter() - t0,
+                                                                        elapsed, args.steps))
     chunks = timed.chunks
     path, nkeys = _native.last_path()
     comb = path == _native.PV_PATH_COMB
