@@ -250,12 +250,22 @@ def ingress_leg(n, blob, off, wire, steps, warmup):
     }
 
 
+def multisig_reduce(bits_nk):
+    """authenticate_multi with threshold None (client_authn.py:84-118) over verdict bits (n, k) in
+    dict order: a request is accepted iff all k signatures verify; a rejected one raises
+    InsufficientCorrectSignatures(k, #correct, {incorrect signers}). Returns (accepted bool[n],
+    correct count int[n])."""
+    return bits_nk.all(axis=1), bits_nk.sum(axis=1)
+
+
 def multisig_leg(multi, n_req, k, steps):
     """configs[3]: n_req requests with k signatures each (authenticate_multi, threshold None = all),
     expanded to one record per (request, signer) and verified in one pv_verify_batch_device call
-    per step; a request is accepted iff all k of its records verify (reduced on the host from the
-    verdict bitmap). Reported beside the headline, never as `value`."""
-    blob, off, pks = multi
+    per step; ~1 % of the records carry a corrupted signature (seeded positions among the k), so the
+    check compares the device's record bitmap with the known bits and the per-request reduction
+    (accepted iff all k verify; #correct of a rejected request) with the expected one. Reported
+    beside the headline, never as `value`."""
+    blob, off, pks, bad = multi
     mb = DeviceBatch(blob, off, pks)
     mb.verify()  # warm-up
     _native.check(_native.lib().pv_sync(), "pv_sync")
@@ -265,14 +275,20 @@ def multisig_leg(multi, n_req, k, steps):
     _native.check(_native.lib().pv_sync(), "pv_sync")
     dt = (time.perf_counter() - t0) / steps
     path, nkeys = _native.last_path()
-    bits = np.unpackbits(mb.verdict_words().view(np.uint8), bitorder="little")[:n_req * k]
-    accepted = int(bits.reshape(n_req, k).all(axis=1).sum())
+    got = bits(mb.verdict_words(), n_req * k).reshape(n_req, k)
     mb.free()
+    acc, correct = multisig_reduce(got)
+    want_acc, want_correct = multisig_reduce(~bad)
+    records_ok = bool(np.array_equal(got, ~bad))
+    reduce_ok = bool(np.array_equal(acc, want_acc) and np.array_equal(correct, want_correct))
     return {"requests": n_req, "signatures_per_request": k, "verifies_per_s": round(n_req * k / dt, 1),
             "requests_per_s": round(n_req / dt, 1), "ms_per_step": round(dt * 1e3, 3), "steps": steps,
-            "distinct_keys": nkeys, "requests_accepted": accepted, "verdicts_ok": accepted == n_req,
+            "distinct_keys": nkeys, "corrupted_records": int(bad.sum()),
+            "requests_accepted": int(acc.sum()), "requests_rejected": int((~acc).sum()),
+            "expected_rejected": int((~want_acc).sum()),
+            "record_bitmap_ok": records_ok, "reduction_ok": reduce_ok, "verdicts_ok": records_ok and reduce_ok,
             "note": "configs[3]: 1 author + 2 endorsers over the same payload, records request-major, "
-                    "device-resident, one launch per step"}
+                    "device-resident, one launch per step; ~1 % of records have a flipped R/S bit"}
 
 
 def config1_python(wire, k=10000):
@@ -610,7 +626,8 @@ def main():
     multi = None
     if world == 1 and not args.no_multisig and not args.dataset:
         t0 = time.perf_counter()
-        multi = nym_workload.generate_multisig(0, min(n, 1 << 20), 3)  # before the device comes up (forked)
+        # before the device comes up (forked); ~1 % corrupted signatures among the 3 per request
+        multi = nym_workload.generate_multisig(0, min(n, 1 << 20), 3, bad_frac=0.01, seed=4)
         log("rank %d: generated %d 3-signature requests in %.1f s" % (rank, min(n, 1 << 20), time.perf_counter() - t0))
 
     # the GPU runtime comes up only after the forked signing workers of the workload generator are

@@ -135,9 +135,14 @@ def _sign_multi_range(args):
     return b"".join(out_sm), [len(x) for x in out_sm], b"".join(out_pk)
 
 
-def generate_multisig(lo, n, k=3, workers=None):
+def generate_multisig(lo, n, k=3, workers=None, bad_frac=0.0, seed=4):
     """configs[3]: requests [lo, lo + n) with k signatures each over the same payload, expanded to
-    one (sig || msg, pk) record per (request, signer), request-major."""
+    one (sig || msg, pk) record per (request, signer), request-major.
+
+    With bad_frac > 0, that fraction of the n * k records (seeded positions, any of a request's k
+    signatures) gets one flipped bit in its signature's R or S half, so libsodium rejects exactly
+    those records. Returns (blob, off, pks, bad) with bad a bool (n, k) array of the corrupted
+    records (all False when bad_frac == 0)."""
     workers = workers or min(16, max(1, (os.cpu_count() or 1)))
     chunk = max(1, (n + workers * 4 - 1) // (workers * 4))
     ranges = [(a, min(a + chunk, lo + n), k) for a in range(lo, lo + n, chunk)]
@@ -149,7 +154,17 @@ def generate_multisig(lo, n, k=3, workers=None):
     blob = np.frombuffer(b"".join(p[0] for p in parts), dtype=np.uint8)
     off = _offsets([x for p in parts for x in p[1]])
     pks = np.frombuffer(b"".join(p[2] for p in parts), dtype=np.uint8).reshape(n * k, 32)
-    return blob, off, pks
+    bad = np.zeros(n * k, bool)
+    if bad_frac > 0:
+        rng = np.random.default_rng(seed)
+        idx = rng.choice(n * k, size=max(1, int(n * k * bad_frac)), replace=False)
+        byte = rng.integers(0, 64, size=len(idx))
+        bit = rng.integers(0, 8, size=len(idx))
+        blob = blob.copy()
+        pos = off[idx].astype(np.int64) + byte
+        blob[pos] ^= (np.uint8(1) << bit.astype(np.uint8))
+        bad[idx] = True
+    return blob, off, pks, bad.reshape(n, k)
 
 
 def _offsets(lens):
