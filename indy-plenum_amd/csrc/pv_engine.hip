@@ -1472,6 +1472,7 @@ struct Ctx {
         std::list<uint32_t> lru;                                                 // slots, most recent first
         std::vector<std::string> slot_key;
         std::vector<uint32_t> free_slots;
+        bool broken = false;  // a failed hash-table upload left the device table stale: not consulted
     } kc;
 };
 
@@ -1492,7 +1493,7 @@ int fail(int code, const std::string& msg) {
 
 PvKeyCacheView kc_view() {
     PvKeyCacheView v{g_ctx.kc.d_htab, g_ctx.kc.d_keys, g_ctx.kc.d_flags, g_ctx.kc.d_tab, 0u, g_ctx.kc.seed};
-    if (g_ctx.kc.enabled && g_ctx.kc.cap > 0 && !g_ctx.kc.index.empty()) v.hmask = g_ctx.kc.hmask;
+    if (g_ctx.kc.enabled && !g_ctx.kc.broken && g_ctx.kc.cap > 0 && !g_ctx.kc.index.empty()) v.hmask = g_ctx.kc.hmask;
     return v;
 }
 
@@ -1505,6 +1506,7 @@ void kc_free() {
     k.d_tab = nullptr;
     k.d_put_pk = nullptr;
     k.cap = k.hmask = 0;
+    k.broken = false;
     k.index.clear();
     k.lru.clear();
     k.slot_key.clear();
@@ -2309,42 +2311,15 @@ int pv_key_cache_configure(uint32_t capacity) {
     return kc_upload_htab(g_ctx.stream);
 }
 
-int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
-    std::lock_guard<std::mutex> lk(g_mu);
+// Builds the fresh keys' tables (slot PV_KC_EMPTY = evicted again within the same put) into their
+// cache slots, in batches of the workspace's comb capacity. PV_TEST_FAIL_KC_PUT_BATCH=b (tests
+// only) reports a failure after batch b has been built and scattered, to exercise the rollback.
+static int kc_build_tables(const std::vector<std::string>& fresh, const std::vector<uint32_t>& fresh_slot) {
     auto& k = g_ctx.kc;
-    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: call pv_init first");
-    if (k.cap == 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: cache not configured");
-    if (n > 0 && !pks) return fail(PV_ERR_ARG, "pv_key_cache_put: null pointer");
-    // slots for the new keys (at most cap of them: the last cap distinct keys of the call win)
-    std::vector<std::string> fresh;
-    std::vector<uint32_t> fresh_slot;
-    for (uint64_t i = 0; i < n; i++) {
-        std::string key(reinterpret_cast<const char*>(pks + 32 * i), 32);
-        auto it = k.index.find(key);
-        if (it != k.index.end()) {  // refresh
-            k.lru.splice(k.lru.begin(), k.lru, it->second);
-            continue;
-        }
-        uint32_t slot;
-        if (!k.free_slots.empty()) {
-            slot = k.free_slots.back();
-            k.free_slots.pop_back();
-        } else {  // evict the least recently put key
-            slot = k.lru.back();
-            k.lru.pop_back();
-            k.index.erase(k.slot_key[slot]);
-            for (size_t f = 0; f < fresh.size(); f++)
-                if (fresh_slot[f] == slot) fresh_slot[f] = PV_KC_EMPTY;  // evicted before it was built
-        }
-        k.lru.push_front(slot);
-        k.index[key] = k.lru.begin();
-        k.slot_key[slot] = key;
-        fresh.push_back(key);
-        fresh_slot.push_back(slot);
-    }
-    // build the new keys' tables in batches of the workspace's comb capacity
     hipStream_t s = g_ctx.stream;
     if (g_ctx.last_stream && g_ctx.last_stream != s) PV_HIP(hipStreamWaitEvent(s, g_ctx.ev_launch_done, 0), PV_ERR_LAUNCH);
+    const char* fail_env = getenv("PV_TEST_FAIL_KC_PUT_BATCH");
+    const long fail_batch = fail_env ? atol(fail_env) : -1;
     KeyWork kw = g_ctx.kw;
     std::vector<uint32_t> ident(kw.kcap);
     for (uint32_t j = 0; j < kw.kcap; j++) ident[j] = j;
@@ -2352,6 +2327,7 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
     PV_HIP(hipMemcpyAsync(kw.key_owner, ident.data(), (uint64_t)kw.kcap * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
     std::vector<uint8_t> bpk;
     std::vector<uint32_t> bslot;
+    long batch = 0;
     for (size_t f0 = 0; f0 < fresh.size();) {
         bpk.clear();
         bslot.clear();
@@ -2381,11 +2357,77 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
                            k.d_put_slot, m, k.d_tab, k.d_flags, k.d_keys);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // bpk / bslot / cnt are host locals
+        if (batch++ == fail_batch) return fail(PV_ERR_LAUNCH, "pv_key_cache_put: injected failure (PV_TEST_FAIL_KC_PUT_BATCH)");
+    }
+    return PV_OK;
+}
+
+int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& k = g_ctx.kc;
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: call pv_init first");
+    if (k.cap == 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: cache not configured");
+    if (n > 0 && !pks) return fail(PV_ERR_ARG, "pv_key_cache_put: null pointer");
+    // slots for the new keys (at most cap of them: the last cap distinct keys of the call win).
+    // The device hash table still holds the state before this call until kc_upload_htab below.
+    std::vector<std::string> fresh;
+    std::vector<uint32_t> fresh_slot, touched;
+    for (uint64_t i = 0; i < n; i++) {
+        std::string key(reinterpret_cast<const char*>(pks + 32 * i), 32);
+        auto it = k.index.find(key);
+        if (it != k.index.end()) {  // refresh
+            k.lru.splice(k.lru.begin(), k.lru, it->second);
+            continue;
+        }
+        uint32_t slot;
+        if (!k.free_slots.empty()) {
+            slot = k.free_slots.back();
+            k.free_slots.pop_back();
+        } else {  // evict the least recently put key
+            slot = k.lru.back();
+            k.lru.pop_back();
+            k.index.erase(k.slot_key[slot]);
+            for (size_t f = 0; f < fresh.size(); f++)
+                if (fresh_slot[f] == slot) fresh_slot[f] = PV_KC_EMPTY;  // evicted before it was built
+        }
+        k.lru.push_front(slot);
+        k.index[key] = k.lru.begin();
+        k.slot_key[slot] = key;
+        fresh.push_back(key);
+        fresh_slot.push_back(slot);
+        touched.push_back(slot);
+    }
+    int rc = kc_build_tables(fresh, fresh_slot);
+    if (rc != PV_OK) {
+        // roll back to a state in which every indexed key's table is built: every slot this call
+        // assigned (its new key's table may be unbuilt, and its evicted key's table may already be
+        // overwritten) leaves the index and returns to the free list; the keys this call did not
+        // touch keep their slots. Then the device hash table is re-uploaded; if even that fails,
+        // the cache is switched off (kc_view() reports it empty) until configure / clear.
+        const std::string err = g_err;
+        std::vector<char> seen(k.cap, 0);
+        for (uint32_t slot : touched) {
+            if (seen[slot]) continue;
+            seen[slot] = 1;
+            auto it = k.index.find(k.slot_key[slot]);
+            if (it != k.index.end() && *it->second == slot) {
+                k.lru.erase(it->second);
+                k.index.erase(it);
+            }
+            k.slot_key[slot].clear();
+            k.free_slots.push_back(slot);
+        }
+        (void)hipStreamSynchronize(g_ctx.stream);
+        if (kc_upload_htab(g_ctx.stream) != PV_OK) k.broken = true;
+        g_err = err;
+        return rc;
     }
     g_ctx.last_keyed = false;
-    PV_HIP(hipEventRecord(g_ctx.ev_launch_done, s), PV_ERR_LAUNCH);
-    g_ctx.last_stream = s;
-    return kc_upload_htab(s);
+    PV_HIP(hipEventRecord(g_ctx.ev_launch_done, g_ctx.stream), PV_ERR_LAUNCH);
+    g_ctx.last_stream = g_ctx.stream;
+    rc = kc_upload_htab(g_ctx.stream);
+    k.broken = rc != PV_OK;  // a complete upload also repairs an earlier failed one
+    return rc;
 }
 
 int pv_key_cache_clear(void) {
@@ -2397,7 +2439,10 @@ int pv_key_cache_clear(void) {
     k.lru.clear();
     k.free_slots.clear();
     for (uint32_t i = k.cap; i-- > 0;) k.free_slots.push_back(i);
-    return kc_upload_htab(g_ctx.stream);
+    for (auto& sk : k.slot_key) sk.clear();
+    const int rc = kc_upload_htab(g_ctx.stream);
+    k.broken = rc != PV_OK;
+    return rc;
 }
 
 int pv_key_cache_enable(int enable) {

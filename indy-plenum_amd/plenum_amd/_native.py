@@ -266,5 +266,7 @@ class KeyCache:
     @staticmethod
     def contains(pk):
         b = np.frombuffer(bytes(pk), np.uint8)
+        if b.size != 32:
+            raise ValueError("keys must be 32 bytes each")
         return bool(lib().pv_key_cache_contains(_ptr(b)))
 

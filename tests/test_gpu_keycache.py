@@ -152,3 +152,36 @@ def test_cached_keys_on_keyed_path(nat, sodium, oracle):
     kc.enable(True)
     kc.clear()
     assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+
+
+def test_put_failure_rolls_back(nat, sodium, oracle, monkeypatch):
+    """A pv_key_cache_put that fails after building part of its keys (injected after the first
+    batch's tables are scattered, over slots that evicted older keys) must leave only keys whose
+    tables are built in the index: every slot the call assigned leaves the cache, the keys it did
+    not touch stay, and verdicts stay libsodium's on every path; a later put succeeds normally."""
+    cases, keys, bad = _batch(sodium, oracle, seed=54, n=900)
+    blob, off, pks = pack(cases)
+    want = _want(sodium, cases)
+    kc = nat.KeyCache
+    kc.configure(16)
+    kc.put(keys[:16])
+    monkeypatch.setenv("PV_TEST_FAIL_KC_PUT_BATCH", "0")
+    with pytest.raises(nat.NativeError, match="injected failure"):
+        kc.put(keys[16:24])  # evicts keys[0:8], builds keys[16:24] into their slots, then "fails"
+    monkeypatch.delenv("PV_TEST_FAIL_KC_PUT_BATCH")
+    assert kc.stats() == (8, 16)
+    assert all(kc.contains(k) for k in keys[8:16])
+    assert not any(kc.contains(k) for k in keys[:8] + keys[16:24])
+    for name in ("latency", "comb", "auto"):
+        nat.set_path(getattr(nat, "PV_PATH_" + name.upper()))
+        got = nat.verify_sm_batch(blob, off, pks)
+        assert np.array_equal(got, want), (name, np.nonzero(got != want)[0][:10])
+    nat.set_path(nat.PV_PATH_AUTO)
+    kc.put(keys[16:24] + bad[:3])
+    assert kc.stats() == (16, 16)  # 8 free slots, then keys[8:11] evicted
+    assert all(kc.contains(k) for k in keys[16:24])
+    nat.set_path(nat.PV_PATH_LATENCY)
+    assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+    nat.set_path(nat.PV_PATH_AUTO)
+    with pytest.raises(ValueError):
+        kc.contains(keys[0][:31])
