@@ -96,25 +96,34 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
 #define PV_STAGE_MSM 3
 #define PV_STAGE_ENCODE 4
 #define PV_NSTAGES 5
-/* Arithmetic path for subsequent launches. Both give bit-identical verdicts:
- *   PV_PATH_STRAUS  per request: decompress A, 9-entry table of [j](-A), regular-window Straus
- *                   double-scalar multiplication (252 doublings + 96 additions)
- *   PV_PATH_COMB    per batch: deduplicate keys; per DISTINCT key: decompress and expand a
- *                   radix-256 comb table; per request: 48 table additions, no doublings (keys
- *                   beyond the PV_KEY_CAP = 16,384 tables a chunk holds take the Straus path)
+/* Arithmetic path for subsequent launches. Every path gives bit-identical verdicts:
+ *   PV_PATH_STRAUS  per request: decompress A, 9-entry table of [j](-A), [S]B from the wide
+ *                   fixed-base comb (11 radix-2^24 lookups: the top entry converted + 10 niels
+ *                   additions), then a regular-window loop over k only: 63 x 4 doublings + 64
+ *                   cached additions, and ONE final addition of [S]B
+ *   PV_PATH_COMB    per batch: deduplicate keys; per DISTINCT key: libsodium's key checks,
+ *                   decompression and a radix-256 comb table T_A[i][d] = [d 256^i](-A) (32 x 129
+ *                   entries); per request: [S]B as above (10 niels additions) and [k](-A) as 32
+ *                   cached table additions, no doublings (keys beyond the PV_KEY_CAP = 16,384 tables
+ *                   a chunk holds take the Straus path in the same launch)
  *   PV_PATH_LATENCY per request: one workgroup (two waves) with limb-parallel arithmetic, every
  *                   field element spread over 10 lanes of a 16-lane row; decompression of A and R in
- *                   one chain, [S]B from the fixed-base comb, [k](-A) by 252 doublings + 64
- *                   additions, and the comparison with R without an inversion. One kernel launch;
- *                   the fastest path for small batches (Plenum's 100 / 1,000-message quotas)
- *   PV_PATH_AUTO    (default) batches of <= 4,096 requests take the latency path, except host
- *                   batches (pv_verify_batch) of 2,049-4,096 requests with >= 3 requests per key
- *                   (counted on the host), which go keyed; otherwise per chunk: deduplicate keys,
- *                   give a comb table to every key with >= 48 requests in the chunk (a table costs
- *                   about what ~50 requests save) -- to every key when the chunk has <= 2,048 keys
- *                   and <= 256k requests -- and verify the other requests on the Straus path in
- *                   the same launch; a tail chunk of <= 4,096 requests goes Straus. Split on the
- *                   device, so pv_verify_batch_device stays asynchronous.
+ *                   one chain, [S]B from the radix-65536 fixed-base comb, [k](-A) by 252 doublings +
+ *                   64 additions (32 table additions for a key in the node-side key cache), and the
+ *                   comparison with R without an inversion. One kernel launch; the fastest path for
+ *                   small batches (Plenum's 100 / 1,000-message quotas)
+ *   PV_PATH_AUTO    (default) batches of <= 2,048 requests take the latency path. From 2,049 to
+ *                   4,096 requests AUTO picks by key repeats: the keyed path with >= 3 requests per
+ *                   key (and <= 2,048 keys), else the latency path; pv_verify_batch counts the keys
+ *                   on the host, pv_verify_batch_device lets its dedup kernels count them and choose
+ *                   on the device (the other path's kernels exit at once; no host round trip). A
+ *                   non-empty key cache keeps such batches on the latency path. Larger batches, per
+ *                   chunk: deduplicate keys, give a comb table to every key with >= 48 requests in
+ *                   the chunk (a table costs about what ~50 requests save) -- to every key when the
+ *                   chunk has <= 2,048 keys and <= 256k requests -- and verify the other requests on
+ *                   the Straus path in the same launch; a tail chunk of <= 4,096 requests goes
+ *                   Straus unless the key cache holds keys (then keyed). Split on the device, so
+ *                   pv_verify_batch_device stays asynchronous.
  * Every path returns bit-identical verdicts. */
 #define PV_PATH_AUTO 0
 #define PV_PATH_STRAUS 1
@@ -137,10 +146,12 @@ int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* laun
  * with 32 additions from the key's radix-256 comb table (660 KB of HBM per key, built once by the
  * engine's key-chain and fill kernels) instead of 252 doublings + 64 additions; verdicts are
  * unchanged (the table holds exact multiples of -A, and libsodium's key checks ran when it was built).
- * Above the latency path's range (AUTO: batches > 4,096 requests) a non-empty cache also makes the
- * launch keyed at any size: a cached key's requests take the comb path at any request count and its
- * table is read from the cache instead of being built (no key chain / table fill for it); uncached
- * keys are handled as without the cache. The benchmark's headline never configures it.
+ * Above the latency path's range (AUTO: batches > 4,096 requests) a non-empty cache also makes every
+ * chunk keyed, the tail chunk of a multi-chunk batch included: a cached key's requests take the comb
+ * path at any request count and its table is read from the cache instead of being built (no key
+ * chain / table fill for it); uncached keys are handled as without the cache. A put that fails part
+ * way (an error from a build step) leaves only keys whose tables were built: every slot the call
+ * assigned is dropped. The benchmark's headline never configures it.
  *   pv_key_cache_configure(capacity)  allocate room for `capacity` keys (0 = free, disabled)
  *   pv_key_cache_put(pks, n)          host keys (n x 32 B): build and insert the missing ones, refresh
  *                                     the present ones; least recently put keys are evicted when full.

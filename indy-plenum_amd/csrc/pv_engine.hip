@@ -104,6 +104,11 @@ static_assert((PV_RANK_SUB & (PV_RANK_SUB - 1)) == 0, "PV_RANK_SUB must be a pow
 #ifndef PV_LATENCY_MAX
 #define PV_LATENCY_MAX 4096  // AUTO: batches up to this size take the latency path (pv_latency.hip)
 #endif
+// AUTO picks latency vs keyed by key repeats from this size up to PV_LATENCY_MAX (pv_keyed_hint on
+// the host, the dedup's lat_choice on the device)
+#ifndef PV_KEYED_HINT_MIN
+#define PV_KEYED_HINT_MIN 2049
+#endif
 
 // ---------------------------------------------------------------------------------------- device
 
@@ -258,10 +263,15 @@ static constexpr int PV_SPLIT_KEYS = 0;        // distinct keys in the chunk
 static constexpr int PV_SPLIT_COMB_KEYS = 1;   // keys given a comb table
 static constexpr int PV_SPLIT_SLOTS = 2;       // requests (slots) of those keys
 static constexpr int PV_SPLIT_SPARSE = 3;      // 1: the comb tables are filled sparsely (small chunk)
+static constexpr int PV_SPLIT_LAT = 4;         // 1: the dedup chose the latency path for this chunk
+static constexpr uint32_t PV_SPLIT_WORDS = 8;  // counters cleared per keyed chunk
 struct Gate {
     const uint32_t* split;
     const uint32_t* slot_req;
     __device__ __forceinline__ bool keyed() const { return split != nullptr; }
+    // the dedup handed this chunk to the latency path (pv_key_scan_kernel, lat_choice): every
+    // kernel of the throughput paths exits at once, the unpermute kernel only cleans up
+    __device__ __forceinline__ bool off() const { return split != nullptr && split[PV_SPLIT_LAT] != 0u; }
     // Straus-path kernels loop over 256-slot tiles t = blockIdx.x, blockIdx.x + gridDim.x, ...;
     // split, the tiles are taken from the END of the slot range (where the Straus slots are) and a
     // small grid strides over them, so the first tile with no Straus slot ends the loop and no
@@ -327,6 +337,7 @@ struct KeyWork {
     uint32_t min_req;
     uint32_t kc_on;    // this launch consults the key cache (pv_key_cache_probe_kernel ran)
     uint32_t chunk_n;  // requests in this chunk
+    uint32_t lat_choice;  // the scan picks latency vs keyed for this chunk (AUTO, device-buffer call)
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 #ifndef PV_COMB_MIN_REQ
@@ -408,6 +419,7 @@ __device__ __forceinline__ void pv_straus_prio() {
 __global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(const uint8_t* __restrict__ sm,
                                                                const uint64_t* __restrict__ off, uint64_t n,
                                                                const uint8_t* __restrict__ pk, Work wk, Gate gate) {
+    if (gate.off()) return;
     pv_straus_prio();
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -420,6 +432,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(co
 
 // Kernel 1b: expand -A (extended, in slot 1) into the cached table [j](-A), j = 0..8.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk, Gate gate) {
+    if (gate.off()) return;
     pv_straus_prio();
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -447,6 +460,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
                                                               const uint64_t* __restrict__ off, uint64_t n,
                                                               const uint32_t* __restrict__ btab_g, Work wk,
                                                               Gate gate) {
+    if (gate.off()) return;
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
     // nothing for this block (or no Straus slot at all): leave before the LDS fill
     if (blockIdx.x >= ntiles || nc >= n || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;
@@ -674,6 +688,10 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
         if (cand_id) j++;
     }
     if (t == 0) {
+        // AUTO's device-side choice for a 2,049..4,096-request batch of pv_verify_batch_device: the
+        // rule pv_keyed_hint applies on the host (>= 3 requests per key, every key a comb key) now
+        // that the dedup has counted the keys; otherwise the latency kernel runs after this chunk
+        kw.nkeys[PV_SPLIT_LAT] = kw.lat_choice && !(nk <= PV_ALLCOMB_KEYS && 3u * nk <= kw.chunk_n) ? 1u : 0u;
         kw.nkeys[PV_SPLIT_COMB_KEYS] = min(ncand, kw.kcap);
         kw.nkeys[PV_SPLIT_SLOTS] = ctotal;
         kw.nkeys[PV_SPLIT_SPARSE] =
@@ -698,11 +716,12 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_scatter_kernel(uint64_t n, Ke
 __global__ __launch_bounds__(PV_BLOCK) void pv_unpermute_kernel(uint64_t n, KeyWork kw, uint64_t* __restrict__ verdict,
                                                                  Gate gate) {
     if (!gate.keyed()) return;
+    const bool lat = gate.off();  // handed to the latency path: zero words for its OR, clean up
     const uint32_t r = blockIdx.x * PV_BLOCK + threadIdx.x;
     bool ok = false;
     if (r < n) {
         const uint32_t s = kw.req_pos[r];
-        ok = (kw.sverdict[s >> 6] >> (s & 63)) & 1;
+        ok = !lat && ((kw.sverdict[s >> 6] >> (s & 63)) & 1);
         // leave the key hash table empty for the next keyed chunk (instead of a 16 MB memset there):
         // every occupied slot is some request's slot
         const uint32_t h = kw.req_key[r];
@@ -892,7 +911,7 @@ __device__ __forceinline__ void pv_chain_prio() {
 // Per distinct key: libsodium's key checks, -A, and the chain of bases [256^i](-A).
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
                                                                     Gate gate) {
-    if (!gate.keyed()) return;
+    if (!gate.keyed() || gate.off()) return;
     pv_chain_prio();
     const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;  // comb index
     if (id >= kw.nkeys[PV_SPLIT_COMB_KEYS] || kw.comb_cslot[id] != PV_EMPTY) return;
@@ -969,7 +988,7 @@ __device__ __forceinline__ void pv_quad_dbl(fe& X, fe& Y, fe& Z, fe& T, const Qu
 // Per distinct key, four lanes: libsodium's key checks, -A, and the bases [256^i](-A), i = 0..31.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_key_chain_quad_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
                                                                          Gate gate) {
-    if (!gate.keyed()) return;
+    if (!gate.keyed() || gate.off()) return;
     // the chain is the batch's critical path and shares SIMDs with the per-request prep kernel:
     // take issue priority over it
     pv_chain_prio();
@@ -1047,7 +1066,7 @@ __device__ __forceinline__ void pv_key_chain_lp(const uint8_t* __restrict__ pk, 
 __global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __restrict__ pk, KeyWork kw, Gate gate,
                                                               int lo, int hi) {
 #if LP_DEVICE
-    if (!gate.keyed()) return;
+    if (!gate.keyed() || gate.off()) return;
     const uint32_t nk = kw.nkeys[PV_SPLIT_COMB_KEYS];
     if (blockIdx.x >= nk) return;
     pv_chain_prio();
@@ -1062,7 +1081,7 @@ __global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __re
 // nkeys * (hi - lo) * 8 items.
 __global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kernel(KeyWork kw, Gate gate, int lo,
                                                                                   int hi) {
-    if (!gate.keyed() || kw.nkeys[PV_SPLIT_SPARSE]) return;
+    if (!gate.keyed() || gate.off() || kw.nkeys[PV_SPLIT_SPARSE]) return;
     const uint32_t np = (uint32_t)(hi - lo);
     const uint32_t items = kw.nkeys[PV_SPLIT_COMB_KEYS] * np * PV_COMB_BLOCKS;
     for (uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x; it < items; it += gridDim.x * PV_BLOCK) {
@@ -1084,7 +1103,7 @@ struct DevNeed {
     __device__ __forceinline__ uint32_t word(int w) const { return p[w]; }
 };
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_fill_sparse_kernel(KeyWork kw, Gate gate) {
-    if (!gate.keyed() || !kw.nkeys[PV_SPLIT_SPARSE]) return;
+    if (!gate.keyed() || gate.off() || !kw.nkeys[PV_SPLIT_SPARSE]) return;
     const uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t id = it / PV_COMB_POS;
     const int pos = (int)(it % PV_COMB_POS);
@@ -1127,7 +1146,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
                                                                     const uint64_t* __restrict__ off, uint64_t n,
                                                                     const uint8_t* __restrict__ pk, Work wk,
                                                                     KeyWork kw, Gate gate) {
-    if (!gate.keyed()) return;
+    if (!gate.keyed() || gate.off()) return;
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
     const uint32_t r = kw.slot_req[i];                         // request
@@ -1198,7 +1217,7 @@ struct DevB2Stage {
 // 0..39.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
                                                                  Gate gate) {
-    if (!gate.keyed()) return;
+    if (!gate.keyed() || gate.off()) return;
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
@@ -1221,6 +1240,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
 // slot range, like the other Straus kernels), extended, to q rows 0..39 for pv_msm_kernel.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_straus_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
                                                                    Gate gate) {
+    if (gate.off()) return;
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
     if (blockIdx.x >= ntiles || nc >= n || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;
     pv_straus_prio();
@@ -1309,7 +1329,7 @@ __device__ __forceinline__ uint32_t pv_xcd_block() {
 // Q to q rows 0..29; the key's own libsodium checks are folded into flags[i] here.
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                Gate gate) {
-    if (!gate.keyed()) return;
+    if (!gate.keyed() || gate.off()) return;
     const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
     const uint32_t id = kw.skey[i];  // comb index
@@ -1398,6 +1418,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* _
                                                                  const uint64_t* __restrict__ off, uint64_t n,
                                                                  Work wk, uint64_t* __restrict__ verdict,
                                                                  KeyWork kw, Gate gate) {
+    if (gate.off()) return;
     const bool comb = gate.keyed();  // slot order
     const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t w = g >> 6, l = g & 63;
@@ -1441,6 +1462,8 @@ struct Ctx {
     bool last_latency = false;  // the most recent launch took the latency path
     bool verdict_zeroed = false;  // the caller's verdict words are already 0 (pv_verify_batch)
     bool keyed_hint = false;      // pv_verify_batch saw few distinct keys: keyed path below PV_LATENCY_MAX
+    bool hint_set = false;        // pv_verify_batch decided keyed_hint on the host (no device-side choice)
+    bool last_dev_choice = false; // the last launch let its dedup pick latency vs keyed
     uint32_t last_split[3] = {0, 0, 0};  // PV_SPLIT_* of it, read back by pv_last_path
     uint4* d_bcomb = nullptr;  // fixed-base comb T_B (radix 65536; latency path)
     uint4* d_bc2 = nullptr;    // wide fixed-base comb T_B2 (radix 2^W; comb path's [S]B)
@@ -1578,10 +1601,19 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
     const uint64_t cap = g_ctx.work.stride;
     const int nchunks = (int)((n + cap - 1) / cap);
     constexpr int NE = PV_NSTAGES + 1;
-    // small batches: one wave pair per request (pv_latency.hip); forced LATENCY takes it at any size
+    // small batches: one wave pair per request (pv_latency.hip); forced LATENCY takes it at any size.
+    // Between PV_KEYED_HINT_MIN and PV_LATENCY_MAX requests AUTO picks by key repeats: the host-buffer
+    // call counted the keys (keyed_hint, hint_set); a device-buffer call lets the dedup kernels count
+    // them and decide on the device (dev_choice: the keyed kernels exit at once and the latency kernel
+    // runs when the scan picks latency; no host round trip). A non-empty key cache keeps the latency
+    // path there (cached keys make it faster still).
+    const bool kc_nonempty = kc_view().hmask != 0;
+    const bool dev_choice = g_ctx.path == PV_PATH_AUTO && !g_ctx.hint_set && !kc_nonempty &&
+                            n >= PV_KEYED_HINT_MIN && n <= PV_LATENCY_MAX;
     const bool latency = g_ctx.path == PV_PATH_LATENCY ||
-                         (g_ctx.path == PV_PATH_AUTO && n <= PV_LATENCY_MAX && !g_ctx.keyed_hint);
+                         (g_ctx.path == PV_PATH_AUTO && n <= PV_LATENCY_MAX && !g_ctx.keyed_hint && !dev_choice);
     g_ctx.last_latency = latency;
+    g_ctx.last_dev_choice = dev_choice;
     int evb = 0;
     if (g_ctx.timing) {
         evb = g_ctx.ev_used;
@@ -1606,7 +1638,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             for (int k = PV_STAGE_PREP; k <= PV_STAGE_MSM; k++)
                 if ((rc = mark(k))) return rc;
             rc = pv_latency_launch(d_sm, d_off + c0, m, d_pk + 32 * c0, g_ctx.d_bcomb, kc_view(),
-                                   d_verdict + c0 / 64, g_ctx.verdict_zeroed, stream);
+                                   d_verdict + c0 / 64, g_ctx.verdict_zeroed, stream, nullptr);
             if (rc) return rc;
             if ((rc = mark(PV_STAGE_ENCODE)) || (rc = mark(PV_NSTAGES))) return rc;
             continue;
@@ -1622,13 +1654,15 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         const PvKeyCacheView kcv = kc_view();
         const bool kc_active = kcv.hmask != 0;
         const bool keyed = g_ctx.path == PV_PATH_COMB ||
-                           (g_ctx.path == PV_PATH_AUTO && (m >= PV_KEYED_MIN || g_ctx.keyed_hint));
+                           (g_ctx.path == PV_PATH_AUTO &&
+                            (m >= PV_KEYED_MIN || g_ctx.keyed_hint || dev_choice || kc_active));
         Gate gate{nullptr, nullptr};
         g_ctx.last_keyed = keyed;
         KeyWork kw = g_ctx.kw;
         kw.min_req = g_ctx.path == PV_PATH_COMB ? 1u : (uint32_t)PV_COMB_MIN_REQ;
         kw.kc_on = kc_active ? 1u : 0u;
         kw.chunk_n = (uint32_t)m;
+        kw.lat_choice = dev_choice ? 1u : 0u;
         kw.kc_tab = g_ctx.kc.d_tab;
         const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
         if (keyed) {
@@ -1642,7 +1676,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                        PV_ERR_LAUNCH);
             }
             g_ctx.slots_dirty = true;  // until this chunk's unpermute kernel is enqueued
-            PV_HIP(hipMemsetAsync(kw.nkeys, 0, 16, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipMemsetAsync(kw.nkeys, 0, PV_SPLIT_WORDS * 4, stream), PV_ERR_LAUNCH);
             if (PV_KEY_SEED > 0 && m > 16ull * PV_KEY_SEED) {  // small chunks: no contention worth a launch
                 const uint64_t ms = std::min<uint64_t>(m, PV_KEY_SEED);
                 hipLaunchKernelGGL(pv_key_seed_kernel, dim3((unsigned)((ms + PV_BLOCK - 1) / PV_BLOCK)), dim3(PV_BLOCK), 0,
@@ -1773,6 +1807,11 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                                d_verdict + c0 / 64, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             g_ctx.slots_dirty = false;
+            if (dev_choice) {  // runs only when the scan picked latency (the words were zeroed above)
+                rc = pv_latency_launch(d_sm, d_off + c0, m, d_pk + 32 * c0, g_ctx.d_bcomb, kc_view(),
+                                       d_verdict + c0 / 64, true, stream, kw.nkeys + PV_SPLIT_LAT);
+                if (rc) return rc;
+            }
         }
         if ((rc = mark(PV_NSTAGES))) return rc;
     }
@@ -1958,14 +1997,15 @@ void pv_shutdown(void) {
 int pv_last_path(int* path, uint32_t* nkeys) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_last_path: call pv_init first");
-    uint32_t u[4] = {0, 0, 0, 0};
+    uint32_t u[PV_SPLIT_WORDS] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (g_ctx.last_keyed) {
         PV_HIP(hipStreamSynchronize(g_ctx.stream), PV_ERR_LAUNCH);
         PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
-        PV_HIP(hipMemcpy(u, g_ctx.kw.nkeys, 12, hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpy(u, g_ctx.kw.nkeys, sizeof(u), hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
     }
     if (nkeys) *nkeys = u[PV_SPLIT_KEYS];
-    if (path) *path = g_ctx.last_latency ? PV_PATH_LATENCY : u[PV_SPLIT_SLOTS] > 0 ? PV_PATH_COMB : PV_PATH_STRAUS;
+    const bool lat = g_ctx.last_latency || (g_ctx.last_keyed && u[PV_SPLIT_LAT] != 0);
+    if (path) *path = lat ? PV_PATH_LATENCY : u[PV_SPLIT_SLOTS] > 0 ? PV_PATH_COMB : PV_PATH_STRAUS;
     g_ctx.last_split[0] = u[PV_SPLIT_KEYS];
     g_ctx.last_split[1] = u[PV_SPLIT_COMB_KEYS];
     g_ctx.last_split[2] = u[PV_SPLIT_SLOTS];
@@ -2132,9 +2172,6 @@ static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* s
 // included (profiles/r02/latency_vs_keyed_crossover.txt): 3,072 requests 0.64 vs 0.71 ms, 4,096
 // 0.65 vs 0.92; at 2 requests per key (2,048) the latency path still wins (0.58 vs 0.61). Keys in
 // the node-side key cache make the latency path faster still: no hint while the cache holds keys.
-#ifndef PV_KEYED_HINT_MIN
-#define PV_KEYED_HINT_MIN 2049
-#endif
 static bool pv_keyed_hint(const uint8_t* pk, uint64_t n) {
     if (g_ctx.path != PV_PATH_AUTO || n < PV_KEYED_HINT_MIN || n > PV_LATENCY_MAX) return false;
     if (g_ctx.kc.enabled && !g_ctx.kc.index.empty()) return false;
@@ -2218,9 +2255,11 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     uint64_t* dver = reinterpret_cast<uint64_t*>(d + pk_bytes + off_bytes);
     g_ctx.verdict_zeroed = true;
     g_ctx.keyed_hint = pv_keyed_hint(pk, n);
+    g_ctx.hint_set = true;
     rc = launch(d + pk_bytes + off_bytes + v_bytes, reinterpret_cast<const uint64_t*>(d + pk_bytes), n, d, dver, s);
     g_ctx.verdict_zeroed = false;
     g_ctx.keyed_hint = false;
+    g_ctx.hint_set = false;
     if (rc) return rc;
     uint64_t* hver = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
     PV_HIP(hipMemcpyAsync(hver, dver, vwords * 8, hipMemcpyDeviceToHost, s), PV_ERR_LAUNCH);
@@ -2340,10 +2379,10 @@ static int kc_build_tables(const std::vector<std::string>& fresh, const std::vec
         f0 = f;
         const uint32_t m = (uint32_t)bslot.size();
         if (m == 0) continue;
-        const uint32_t cnt[4] = {m, m, 0, 0};  // keys, comb keys, slots, sparse = 0: every table in full
+        const uint32_t cnt[PV_SPLIT_WORDS] = {m, m, 0, 0, 0, 0, 0, 0};  // keys, comb keys; sparse, lat = 0
         PV_HIP(hipMemcpyAsync(k.d_put_pk, bpk.data(), bpk.size(), hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemcpyAsync(k.d_put_slot, bslot.data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-        PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, 16, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, sizeof(cnt), hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
         PV_HIP(hipMemsetAsync(kw.comb_cslot, 0xFF, (uint64_t)m * 4, s), PV_ERR_LAUNCH);  // build every table
         const Gate gate{kw.nkeys, kw.slot_req};
         hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(m, PV_LP_CHAIN_BLOCKS)), dim3(64), 0, s,

@@ -48,8 +48,10 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
                                                               const uint64_t* __restrict__ off, uint64_t n,
                                                               const uint8_t* __restrict__ pk,
                                                               const uint32_t* __restrict__ bcomb, PvKeyCacheView kc,
-                                                              unsigned long long* __restrict__ verdict) {
+                                                              unsigned long long* __restrict__ verdict,
+                                                              const uint32_t* __restrict__ run_if) {
 #if LP_DEVICE  // the lp types are 64-lane host arrays in the host pass: the body is device-only
+    if (run_if && *run_if == 0u) return;  // AUTO's device-side choice picked the keyed path
     const uint32_t r = blockIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 // Enqueue the latency path for n requests (device buffers as pv_verify_batch_device) on `stream`.
 int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
                       const void* d_bcomb, const PvKeyCacheView& kc, uint64_t* d_verdict, bool verdict_zeroed,
-                      hipStream_t stream) {
+                      hipStream_t stream, const uint32_t* run_if) {
     if (n == 0) return PV_OK;
     if (n > 0x7FFFFFFFull) return pv_fail(PV_ERR_ARG, "pv_latency: too many requests for one launch");
     hipError_t e = hipSuccess;
@@ -157,7 +159,8 @@ int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, co
         if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
     }
     hipLaunchKernelGGL(pv_lat_kernel, dim3((unsigned)n), dim3(LAT_THREADS), 0, stream, d_sm, d_off, n, d_pk,
-                       reinterpret_cast<const uint32_t*>(d_bcomb), kc, reinterpret_cast<unsigned long long*>(d_verdict));
+                       reinterpret_cast<const uint32_t*>(d_bcomb), kc, reinterpret_cast<unsigned long long*>(d_verdict),
+                       run_if);
     e = hipGetLastError();
     if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("pv_lat_kernel: ") + hipGetErrorString(e));
     return PV_OK;

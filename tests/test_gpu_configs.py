@@ -338,3 +338,34 @@ def test_medium_host_batch_path_hint(native, sodium):
             got = native.verify_sm_batch(blob, off, pks)
             native.set_path(native.PV_PATH_AUTO)
             assert np.array_equal(got, want), (forced, np.nonzero(got != want)[0][:10])
+
+
+def test_medium_device_batch_path_choice(native, sodium):
+    """The device-buffer twin of test_medium_host_batch_path_hint: pv_verify_batch_device cannot
+    count keys on the host, so for 2,049..4,096 requests AUTO runs the dedup kernels and lets the
+    scan pick (>= 3 requests per key: keyed; else the latency kernel runs and the keyed kernels exit
+    at once). Same paths and bit-exact verdicts as the host-buffer call; verdict words that held
+    stale bits before the call are fully rewritten on both outcomes."""
+    from bench import DeviceBatch, bits
+    from oracle.oracle import cpu_verdicts
+    native.set_path(native.PV_PATH_AUTO)
+    for n_signed, n_single, want_path in ((4096, 0, native.PV_PATH_COMB), (3072, 0, native.PV_PATH_COMB),
+                                          (2048, 8, native.PV_PATH_LATENCY),
+                                          (0, 3000, native.PV_PATH_LATENCY), (0, 4096, native.PV_PATH_LATENCY)):
+        blob, off, pks = _split_batch(sodium, n_signed, n_single, seed=41 + n_signed + n_single)
+        n = len(off) - 1
+        want = cpu_verdicts(blob, off, pks)
+        db = DeviceBatch(blob, off, pks)
+        try:
+            stale = np.full(db.words, 0xA5A5A5A5A5A5A5A5, np.uint64)
+            native.check(native.lib().pv_memcpy_h2d(db.d_verdict, stale.ctypes.data, stale.nbytes), "h2d")
+            db.verify()
+            got = bits(db.verdict_words(), n)
+            path, _ = native.last_path()
+            assert path == want_path, (n_signed, n_single, path)
+            assert np.array_equal(got, want), (n_signed, n_single, np.nonzero(got != want)[0][:10])
+            # the next launch on the same workspace (the other outcome) still sees a clean table
+            db.verify()
+            assert np.array_equal(bits(db.verdict_words(), n), want)
+        finally:
+            db.free()
