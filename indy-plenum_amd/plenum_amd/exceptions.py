@@ -151,3 +151,15 @@ class InvalidNodeMsg(InvalidNodeMessageException):
 class InvalidClientRequest(InvalidClientMessageException):
     pass
 
+
+
+class MissingNodeOp(InvalidNodeMsg):
+    pass
+
+
+class InvalidNodeOp(InvalidNodeMsg):
+    pass
+
+
+class InvalidClientMsgType(InvalidClientRequest):
+    pass

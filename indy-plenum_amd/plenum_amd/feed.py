@@ -25,28 +25,38 @@ side effects to the caller (sending the NACK, reporting the node, queueing the m
 
 Static validation of client requests (Node.doStaticValidation, node.py:1651-1652: request handlers,
 out of scope here) is the caller's `static_validation(request)` hook, run where the reference runs
-it (after the Request is built, before the signature check). The PROPAGATE message schema
-(node_message_factory.get_instance, node.py:1494) is the caller's `message_factory(msg)` hook; by
-default a message is accepted as a PROPAGATE when it is a dict with op == "PROPAGATE" and a dict
-"request".
+it (after the Request is built, before the signature check). A client message carrying "op" is
+routed as validateClientMsg routes it (node.py:1634-1638): Batch / LedgerStatus / CatchupReq are
+NotARequest (the node's own handler takes them), any other registered op is NACKed with
+InvalidClientMsgType(cls, reqId), an unknown op with InvalidNodeOp. A node message goes through
+validateNodeMsg's construction step (node.py:1492-1498) with node_messages.MessageFactory: the
+registry (MissingNodeOp / InvalidNodeOp) and Propagate's own schema (missing fields, the request
+body's type, senderClient), the reference's exception texts wrapped into InvalidNodeMsg as the
+node does; the request body's full schema (ClientMessageValidator) is the factory's
+`request_schema` hook, or the whole factory is replaced through `message_factory(msg)` (e.g. the
+reference's node_message_factory.get_instance). A message of another registered op is
+NotAPropagate (the node's own handleOneNodeMsg takes it).
 """
 import re
 from collections import namedtuple
 
 from .constants import IDENTIFIER, OPERATION, REQ_ID, SIGNATURES
-from .exceptions import BaseExc, InvalidClientRequest, InvalidNodeMsg
+from .exceptions import BaseExc, InvalidClientMsgType, InvalidClientRequest
+from .node_messages import CLIENT_OPS, OP_FIELD_NAME, MessageFactory, NodeMessageType, validate_node_message
 from .wire import Request
 
-OP_FIELD_NAME = "op"          # plenum/common/constants.py OP_FIELD_NAME
 PROPAGATE = "PROPAGATE"       # plenum/common/constants.py PROPAGATE
+NODE_MESSAGE_FACTORY = MessageFactory()
 
 # a request that passed: what handleOneClientMsg hands to unpackClientMsg (node.py:1566-1567)
 ClientAccepted = namedtuple("ClientAccepted", "request frm identifiers")
 # what handleInvalidClientMsg sends: send_nack_to_client((identifier, reqId), reason, frm)
 ClientNack = namedtuple("ClientNack", "frm identifier req_id reason exc")
-# a client message with an 'op' field (Batch / LedgerStatus / CatchupReq): not a request, the node's
-# other branch of validateClientMsg (node.py:1634-1638) handles it
+# a client message whose 'op' is Batch / LedgerStatus / CatchupReq: not a request, the node's other
+# branch of validateClientMsg (node.py:1634-1638) handles it
 NotARequest = namedtuple("NotARequest", "msg frm")
+# a node message of a registered op other than PROPAGATE: the node's own handleOneNodeMsg takes it
+NotAPropagate = namedtuple("NotAPropagate", "msg frm")
 # handleOneClientMsg itself raised (a non-dict message: handleInvalidClientMsg's msg.get fails)
 ClientError = namedtuple("ClientError", "msg frm exc")
 PropagateAccepted = namedtuple("PropagateAccepted", "message frm request identifiers")
@@ -99,6 +109,9 @@ def _client_request(msg, cls, static_validation):
     if all([msg.get(OPERATION), msg.get(REQ_ID), idr_from_req_data(msg)]):
         need_static = True
     elif OP_FIELD_NAME in msg:
+        cls = NODE_MESSAGE_FACTORY.get_type(msg[OP_FIELD_NAME])  # InvalidNodeOp / TypeError propagate
+        if cls not in CLIENT_OPS:
+            raise InvalidClientMsgType(cls, msg.get(REQ_ID))
         return None
     else:
         raise InvalidClientRequest(msg.get(IDENTIFIER), msg.get(REQ_ID))
@@ -174,16 +187,21 @@ def _suspicious(frm, ex, message):
 
 
 def _default_propagate(msg):
-    if not isinstance(msg, dict) or msg.get(OP_FIELD_NAME) != PROPAGATE or not isinstance(msg.get("request"), dict):
-        raise InvalidNodeMsg("not a PROPAGATE: {}".format(str(msg)[:64]))
-    return msg
+    return validate_node_message(NODE_MESSAGE_FACTORY, msg)
+
+
+def _is_propagate(message):
+    if isinstance(message, NodeMessageType):
+        return False
+    return isinstance(message, dict) or getattr(message, "typename", PROPAGATE) == PROPAGATE
 
 
 def authenticate_propagates(req_authnr, wrapped, message_factory=_default_propagate, request_class=Request,
                             engine=None):
-    """The PROPAGATE messages of a node Batch [(msg dict, frm)] -> one outcome per message, all
-    signatures in one engine launch: PropagateAccepted, the SuspiciousNode the node reports, or
-    PropagateDiscarded with the exception the node discards the message for."""
+    """The messages of a node Batch [(msg dict, frm)] -> one outcome per message, all PROPAGATE
+    signatures in one engine launch: PropagateAccepted, the SuspiciousNode the node reports,
+    PropagateDiscarded with the exception the node discards the message for, or NotAPropagate for a
+    message of another registered op."""
     outcomes = [None] * len(wrapped)
     live = []  # (index, message, request, (req_dict, key))
     for i, (msg, frm) in enumerate(wrapped):
@@ -191,6 +209,9 @@ def authenticate_propagates(req_authnr, wrapped, message_factory=_default_propag
             message = message_factory(msg)
         except Exception as ex:  # validateNodeMsg: InvalidNodeMsg and friends propagate (node.py:1493-1498)
             outcomes[i] = PropagateDiscarded(msg, frm, ex)
+            continue
+        if not _is_propagate(message):
+            outcomes[i] = NotAPropagate(msg, frm)
             continue
         try:
             request = message["request"] if isinstance(message, dict) else message.request

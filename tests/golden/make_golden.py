@@ -366,7 +366,7 @@ def _node_methods():
     cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Node")
     want = {"handleOneClientMsg", "validateClientMsg", "handleInvalidClientMsg",
             "_specific_invalid_client_msg_handling", "handleOneNodeMsg", "validateNodeMsg", "verifySignature",
-            "authNr"}
+            "authNr", "white_list_init"}
     funcs = [fn for fn in cls.body if isinstance(fn, ast.FunctionDef) and fn.name in want]
     assert {fn.name for fn in funcs} == want
     for fn in funcs:
@@ -384,7 +384,9 @@ def _node_methods():
         def __getattr__(self, name):
             return name
 
-    ns = dict(f=f, OPERATION=OPERATION, OP_FIELD_NAME=OP_FIELD_NAME, LEDGER_STATUS=LEDGER_STATUS, Batch=Batch,
+    from plenum.common.messages import node_messages as NM
+    ns = {n: getattr(NM, n) for n in dir(NM) if not n.startswith("_")}  # white_list_init's classes
+    ns.update(f=f, OPERATION=OPERATION, OP_FIELD_NAME=OP_FIELD_NAME, LEDGER_STATUS=LEDGER_STATUS, Batch=Batch,
               LedgerStatus=LedgerStatus, CatchupReq=CatchupReq, Propagate=Propagate,
               node_message_factory=node_message_factory, PreSigVerification=PreSigVerification,
               TxnUtilConfig=TxnUtilConfig, idr_from_req_data=idr_from_req_data, friendlyEx=friendlyEx,
@@ -397,12 +399,12 @@ def _node_methods():
 class _StubNode:
     """What the feed-point methods touch on a Node; records the side effects."""
 
-    def __init__(self, methods, metrics_cls, whitelist, req_authnr):
+    def __init__(self, methods, metrics_cls, req_authnr):
         import types
         for name, fn in methods.items():
             setattr(self, name, types.MethodType(fn, self))
         self.metrics = metrics_cls()
-        self.authnWhitelist = whitelist
+        self.white_list_init()  # the node's own authnWhitelist (node.py:405-431)
         self.clientAuthNr = req_authnr
         self.client_request_class = Request
         self.events = []
@@ -428,7 +430,7 @@ class _StubNode:
         pass
 
     def unpackClientMsg(self, msg, frm):
-        self.events.append({"ev": "accepted", "frm": frm})
+        self.events.append({"ev": "accepted", "frm": frm, "type": type(msg).__name__})
 
     def send_nack_to_client(self, idr_reqid, reason, frm):
         self.events.append({"ev": "nack", "frm": frm, "identifier": idr_reqid[0], "reqId": idr_reqid[1],
@@ -445,7 +447,7 @@ class _StubNode:
                             "cause": type(ex.__cause__).__name__, "cause_str": str(ex.__cause__)})
 
     def unpackNodeMsg(self, msg, frm):
-        self.events.append({"ev": "accepted", "frm": frm})
+        self.events.append({"ev": "accepted", "frm": frm, "type": type(msg).__name__})
 
     def _invalid_client_ledger_status_handling(self, ex, msg, frm):
         pass
@@ -502,11 +504,26 @@ def gen_feed():
     r["self"] = 1
     reqs.append(("bad_kwarg", r))
     reqs.append(("not_a_dict", [1, 2, 3]))
+    # messages carrying "op" (validateClientMsg's second branch, node.py:1634-1638)
+    ls = {"op": "LEDGER_STATUS", "ledgerId": 1, "txnSeqNo": 10, "viewNo": None, "ppSeqNo": None,
+          "merkleRoot": base58.b58encode(bytes(range(32))).decode(), "protocolVersion": 2}
+    reqs.append(("op_ledger_status", ls))
+    reqs.append(("op_ledger_status_bad", {"op": "LEDGER_STATUS", "ledgerId": "x", "reqId": 77}))
+    reqs.append(("op_catchup_req", {"op": "CATCHUP_REQ", "ledgerId": 1, "seqNoStart": 1, "seqNoEnd": 5,
+                                    "catchupTill": 5}))
+    reqs.append(("op_batch", {"op": "BATCH", "messages": [], "signature": None}))
+    reqs.append(("op_propagate", {"op": "PROPAGATE", "request": signed_request(signers[0], 121),
+                                  "senderClient": "cli0"}))
+    reqs.append(("op_prepare", {"op": "PREPARE", "instId": 0, "viewNo": 0, "ppSeqNo": 1, "ppTime": 1,
+                                "digest": "d", "stateRootHash": None, "txnRootHash": None, "reqId": 9}))
+    reqs.append(("op_unknown", {"op": "FOO", "reqId": 5, "identifier": signers[0].identifier}))
+    reqs.append(("op_unhashable", {"op": ["x"], "identifier": signers[1].identifier}))
+    reqs.append(("op_none", {"op": None}))
     frms = ["cli%d" % (i % 3) for i in range(len(reqs))]
 
     # client quota: handleOneClientMsg per message, in order, one node
     ra, core, spy = fresh_authnr()
-    node = _StubNode(methods, metrics_cls, (Batch,), ra)
+    node = _StubNode(methods, metrics_cls, ra)
     client = []
     for (label, msg), frm in zip(reqs, frms):
         node.events.clear()
@@ -522,13 +539,32 @@ def gen_feed():
                        "authenticate_calls": spy["calls"] - before})
     # PROPAGATEs of a node Batch: handleOneNodeMsg per message
     ra, core, spy = fresh_authnr()
-    node = _StubNode(methods, metrics_cls, (Batch,), ra)
+    node = _StubNode(methods, metrics_cls, ra)
     props = []
+    nodemsgs = []
     for j, (label, msg) in enumerate(reqs):
-        if label in ("not_a_dict", "no_reqid", "bad_kwarg"):
+        if label in ("not_a_dict", "no_reqid", "bad_kwarg") or label.startswith("op_"):
             continue
+        nodemsgs.append((label, {"op": "PROPAGATE", "request": msg, "senderClient": "client%d" % j}))
+    good = signed_request(signers[1], 130)
+    # node messages that are not well-formed PROPAGATEs (validateNodeMsg, node.py:1492-1498)
+    nodemsgs += [("prop_missing_request", {"op": "PROPAGATE", "senderClient": "c1"}),
+                 ("prop_missing_sender", {"op": "PROPAGATE", "request": good}),
+                 ("prop_sender_none", {"op": "PROPAGATE", "request": good, "senderClient": None}),
+                 ("prop_sender_int", {"op": "PROPAGATE", "request": good, "senderClient": 5}),
+                 ("prop_sender_empty", {"op": "PROPAGATE", "request": good, "senderClient": ""}),
+                 ("prop_sender_long", {"op": "PROPAGATE", "request": good, "senderClient": "x" * 300}),
+                 ("prop_request_list", {"op": "PROPAGATE", "request": [1, 2], "senderClient": "c1"}),
+                 ("prop_extra_field", {"op": "PROPAGATE", "request": good, "senderClient": "c1", "extra": 1}),
+                 ("prop_unknown_op", {"op": "PROPAGATEX", "request": good, "senderClient": "c1"}),
+                 ("prop_missing_op", {"request": good, "senderClient": "c1"}),
+                 ("prop_none_op", {"op": None, "request": good, "senderClient": "c1"}),
+                 ("prop_unhashable_op", {"op": {"a": 1}, "request": good, "senderClient": "c1"}),
+                 ("node_prepare", {"op": "PREPARE", "instId": 0, "viewNo": 0, "ppSeqNo": 1, "ppTime": 1,
+                                   "digest": "d", "stateRootHash": None, "txnRootHash": None}),
+                 ("node_not_a_dict", [1, 2])]
+    for j, (label, pm) in enumerate(nodemsgs):
         frm = ["Node2", "Node3:9702", "Node4"][j % 3]
-        pm = {"op": "PROPAGATE", "request": msg, "senderClient": "client%d" % j}
         node.events.clear()
         try:
             node.handleOneNodeMsg((json.loads(json.dumps(pm)), frm))
@@ -536,7 +572,9 @@ def gen_feed():
         except Exception as ex:
             raised = {"exc": type(ex).__name__, "msg": str(ex)}
         props.append({"label": label, "msg": pm, "frm": frm, "events": list(node.events), "raised": raised})
-    return {"clients": clients, "client_quota": client, "propagates": props}
+    from plenum.common.messages.node_message_factory import node_message_factory
+    registry = {k: repr(v) for k, v in node_message_factory._MessageFactory__classes.items()}
+    return {"clients": clients, "client_quota": client, "propagates": props, "node_message_registry": registry}
 
 
 GENERATORS = {"serializer.json": lambda: gen_serializer(), "didverifier.json": lambda: gen_didverifier(),
