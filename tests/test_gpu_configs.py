@@ -90,6 +90,7 @@ def test_config4_multisig(native, sodium):
     db = DeviceBatch(blob, off, pk)
     try:
         db.verify()
+        native.check(native.lib().pv_sync(), "pv_sync")  # the copy-back is not ordered after the engine stream
         assert np.array_equal(bits(db.verdict_words(), n_req * k).reshape(n_req, k), want)
     finally:
         db.free()
@@ -360,12 +361,14 @@ def test_medium_device_batch_path_choice(native, sodium):
             stale = np.full(db.words, 0xA5A5A5A5A5A5A5A5, np.uint64)
             native.check(native.lib().pv_memcpy_h2d(db.d_verdict, stale.ctypes.data, stale.nbytes), "h2d")
             db.verify()
+            native.check(native.lib().pv_sync(), "pv_sync")
             got = bits(db.verdict_words(), n)
             path, _ = native.last_path()
             assert path == want_path, (n_signed, n_single, path)
             assert np.array_equal(got, want), (n_signed, n_single, np.nonzero(got != want)[0][:10])
             # the next launch on the same workspace (the other outcome) still sees a clean table
             db.verify()
+            native.check(native.lib().pv_sync(), "pv_sync")
             assert np.array_equal(bits(db.verdict_words(), n), want)
         finally:
             db.free()
