@@ -160,13 +160,25 @@ int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* laun
  *   pv_key_cache_clear()              drop every key (capacity kept)
  *   pv_key_cache_enable(on)           whether launches consult the cache (default on)
  *   pv_key_cache_stats(size, cap)     keys held / capacity
- *   pv_key_cache_contains(pk)         1 if the 32-byte key is cached */
+ *   pv_key_cache_contains(pk)         1 if the 32-byte key is cached
+ *   pv_key_cache_auto(min_seen)       automatic admission (0 = off, the default): pv_verify_batch calls
+ *                                     of <= 4,096 requests count their keys, and a key seen min_seen
+ *                                     times within the counting window (the last ~32k distinct keys) is
+ *                                     put into the cache right behind that batch on the engine stream
+ *                                     -- the call waits only for its own verdicts, the table build
+ *                                     (~1 ms) overlaps the caller's next steps and the next launch is
+ *                                     ordered after it. A failed admission leaves the verdicts
+ *                                     unchanged and the keys uncached. Verkeys come from NYM records
+ *                                     (plenum/server/request_handlers/utils.py:30-39): signers repeat
+ *   pv_key_cache_auto_stats(a, f)     keys admitted automatically / admissions that failed */
 int pv_key_cache_configure(uint32_t capacity);
 int pv_key_cache_put(const uint8_t* pks, uint64_t n);
 int pv_key_cache_clear(void);
 int pv_key_cache_enable(int enable);
 int pv_key_cache_stats(uint32_t* size, uint32_t* capacity);
 int pv_key_cache_contains(const uint8_t* pk);
+int pv_key_cache_auto(uint32_t min_seen);
+int pv_key_cache_auto_stats(uint64_t* admitted, uint64_t* failed);
 
 /* Batched base58 decode (Bitcoin alphabet, PyPI base58 2.x b58decode semantics: trailing ASCII
  * whitespace stripped, each leading '1' -> 0x00). Input: strings concatenated in `chars` with

@@ -264,7 +264,8 @@ static constexpr int PV_SPLIT_COMB_KEYS = 1;   // keys given a comb table
 static constexpr int PV_SPLIT_SLOTS = 2;       // requests (slots) of those keys
 static constexpr int PV_SPLIT_SPARSE = 3;      // 1: the comb tables are filled sparsely (small chunk)
 static constexpr int PV_SPLIT_LAT = 4;         // 1: the dedup chose the latency path for this chunk
-static constexpr uint32_t PV_SPLIT_WORDS = 8;  // counters cleared per keyed chunk
+static constexpr int PV_SPLIT_QUEUE = 8;       // [8..15]: pv_comb_a_kernel's per-XCD tile counters
+static constexpr uint32_t PV_SPLIT_WORDS = 16; // counters cleared per keyed chunk
 struct Gate {
     const uint32_t* split;
     const uint32_t* slot_req;
@@ -1141,6 +1142,18 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_kc_scatter_kernel(const uint4* __
     }
 }
 
+// Key cache put: the workspace set up for m keys given in order (d_put_pk[j] is comb index j's key):
+// identity key ids, no cached table, split counters {m keys, m comb keys, everything else 0}.
+__global__ __launch_bounds__(PV_BLOCK) void pv_kc_put_prep_kernel(KeyWork kw, uint32_t m) {
+    const uint32_t j = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (j < PV_SPLIT_WORDS) kw.nkeys[j] = (j == PV_SPLIT_KEYS || j == PV_SPLIT_COMB_KEYS) ? m : 0u;
+    if (j < m) {
+        kw.comb_key[j] = j;
+        kw.key_owner[j] = j;
+        kw.comb_cslot[j] = PV_EMPTY;
+    }
+}
+
 // Per request on the comb path: signature checks, k, key id and validity, radix-256 digits of k, S.
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t* __restrict__ sm,
                                                                     const uint64_t* __restrict__ off, uint64_t n,
@@ -1327,11 +1340,7 @@ __device__ __forceinline__ uint32_t pv_xcd_block() {
 
 // Second half: Q = acc + [k](-A) from the key's comb table (32 additions, no doublings), projective
 // Q to q rows 0..29; the key's own libsodium checks are folded into flags[i] here.
-__global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
-                                                                               Gate gate) {
-    if (!gate.keyed() || gate.off()) return;
-    const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
-    if (i >= gate.ncomb()) return;
+__device__ __forceinline__ void pv_comb_a_slot(const Work& wk, const KeyWork& kw, uint32_t i, uint4* stg_wave) {
     const uint32_t id = kw.skey[i];  // comb index
     const uint32_t cslot = kw.comb_cslot[id];
     const uint4* ktab = cslot != PV_EMPTY ? kw.kc_tab + (uint64_t)cslot * PV_COMB_POS * PV_COMB_ENT * 10
@@ -1349,9 +1358,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
     const DevDigits dig{wk.digits, S, i};
     fe X, Y, Z;
 #if PV_COMB_PIPELINE
-    __shared__ uint4 stg[PV_BLOCK / 64][10][64];
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    pv_comb_a_xyz_staged(X, Y, Z, acc, DevCombStage{ktab, &stg[wv][0][0], threadIdx.x & 63u}, dig);
+    pv_comb_a_xyz_staged(X, Y, Z, acc, DevCombStage{ktab, stg_wave, threadIdx.x & 63u}, dig);
 #else
     const DevCombRows arows{const_cast<uint4*>(ktab)};
     pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
@@ -1363,6 +1370,47 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
         qs.st(10 + q, i, Y.v[q]);
         qs.st(20 + q, i, Z.v[q]);
     }
+}
+
+// Tile scheduling of pv_comb_a_kernel. PV_COMB_A_QUEUE = 1: a resident grid (4 workgroups per CU)
+// takes 256-slot tiles from per-XCD work queues (atomic counters in nkeys[PV_SPLIT_QUEUE + x]): XCD
+// x owns a contiguous range of the key-sorted tiles (a key's table rows stay in its L2) and, once
+// its range is drained, helps the other XCDs. Nothing is quantised into rounds of the chip's 1,024
+// workgroup slots, so the few slots a split chunk's Straus-side waves hold (config 3) cost only
+// their share of the work instead of a fifth partial round. 0: one workgroup per tile, XCD-remapped.
+#ifndef PV_COMB_A_QUEUE
+#define PV_COMB_A_QUEUE 1
+#endif
+__global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
+                                                                               Gate gate) {
+    if (!gate.keyed() || gate.off()) return;
+    __shared__ uint4 stg[PV_BLOCK / 64][10][64];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nc = gate.ncomb();
+#if PV_COMB_A_QUEUE
+    __shared__ uint32_t s_tile;
+    const uint32_t ntiles = (nc + PV_BLOCK - 1) / PV_BLOCK;
+    const uint32_t q = ntiles >> 3, r = ntiles & 7;
+    const uint32_t home = blockIdx.x & 7;  // workgroups are dispatched to the XCDs round-robin
+    for (uint32_t probe = 0; probe < 8; probe++) {
+        const uint32_t x = (home + probe) & 7;
+        const uint32_t lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+        const uint32_t cnt = q + (x < r ? 1u : 0u);
+        for (;;) {
+            __syncthreads();  // every wave is done with s_tile and the staging area
+            if (threadIdx.x == 0) s_tile = atomicAdd(&kw.nkeys[PV_SPLIT_QUEUE + x], 1u);
+            __syncthreads();
+            const uint32_t t = s_tile;
+            if (t >= cnt) break;  // uniform over the workgroup: every wave leaves this range together
+            const uint32_t i = (lo + t) * PV_BLOCK + threadIdx.x;  // slot
+            if (i < nc) pv_comb_a_slot(wk, kw, i, &stg[wv][0][0]);
+        }
+    }
+#else
+    const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
+    if (i >= nc) return;
+    pv_comb_a_slot(wk, kw, i, &stg[wv][0][0]);
+#endif
 }
 
 // Kernel 3: encode Q for PV_ENC_BATCH requests per lane with one shared inversion, compare with R,
@@ -1453,6 +1501,7 @@ struct Ctx {
     // on its stream; a launch on a DIFFERENT stream first makes its stream wait for it, so two
     // batches enqueued on two caller streams never share the workspace at the same time.
     hipEvent_t ev_launch_done = nullptr;
+    hipEvent_t ev_verdict_copied = nullptr;  // pv_verify_batch: verdicts back (an admission may follow)
     hipStream_t last_stream = nullptr;
     uint32_t* d_btab = nullptr;
     Work work{nullptr, nullptr, nullptr, nullptr, 0};
@@ -1496,6 +1545,20 @@ struct Ctx {
         std::vector<std::string> slot_key;
         std::vector<uint32_t> free_slots;
         bool broken = false;  // a failed hash-table upload left the device table stale: not consulted
+        // automatic admission (pv_key_cache_auto): a key is put on its auto_min-th appearance in
+        // pv_verify_batch calls of <= PV_KC_AUTO_MAX_BATCH requests. Appearances are counted in an
+        // open-addressing table of full keys (seen_cnt 255 = admitted), cleared when half full:
+        // the counting window is the last ~PV_KC_SEEN_H / 2 distinct keys
+        uint32_t auto_min = 0;
+        std::vector<uint64_t> seen_key;  // [PV_KC_SEEN_H][4]
+        std::vector<uint8_t> seen_cnt;   // [PV_KC_SEEN_H]
+        uint32_t seen_used = 0;
+        uint64_t auto_admitted = 0, auto_failed = 0;
+        // pinned staging of an asynchronous put (keys, slots, hash table), reused once ev_async is done
+        uint8_t* h_async = nullptr;
+        uint64_t h_async_cap = 0;
+        hipEvent_t ev_async = nullptr;
+        bool async_pending = false;
     } kc;
 };
 
@@ -1528,18 +1591,34 @@ void kc_free() {
     k.d_htab = k.d_keys = k.d_flags = k.d_put_slot = nullptr;
     k.d_tab = nullptr;
     k.d_put_pk = nullptr;
+    if (k.async_pending && k.ev_async) (void)hipEventSynchronize(k.ev_async);
+    k.async_pending = false;
+    if (k.h_async) (void)hipHostFree(k.h_async);
+    k.h_async = nullptr;
+    k.h_async_cap = 0;
     k.cap = k.hmask = 0;
     k.broken = false;
+    k.seen_used = 0;
+    std::fill(k.seen_cnt.begin(), k.seen_cnt.end(), 0);
     k.index.clear();
     k.lru.clear();
     k.slot_key.clear();
     k.free_slots.clear();
 }
 
-// Rebuild the open-addressing table from the index and upload it (stream-ordered).
-int kc_upload_htab(hipStream_t s) {
+// Rebuild the open-addressing table from the index and upload it (stream-ordered). hbuf: pinned
+// room for hmask + 1 words whose copy the caller lets run asynchronously; nullptr = a local buffer
+// and a synchronous upload.
+int kc_upload_htab(hipStream_t s, uint32_t* hbuf = nullptr) {
     auto& k = g_ctx.kc;
-    std::vector<uint32_t> h((size_t)k.hmask + 1, PV_KC_EMPTY);
+    std::vector<uint32_t> local;
+    uint32_t* h = hbuf;
+    if (!h) {
+        local.assign((size_t)k.hmask + 1, PV_KC_EMPTY);
+        h = local.data();
+    } else {
+        std::fill(h, h + k.hmask + 1, PV_KC_EMPTY);
+    }
     for (auto& e : k.index) {
         uint32_t A[8];
         memcpy(A, e.first.data(), 32);
@@ -1547,8 +1626,8 @@ int kc_upload_htab(hipStream_t s) {
         while (h[p] != PV_KC_EMPTY) p = (p + 1) & k.hmask;
         h[p] = *e.second;
     }
-    PV_HIP(hipMemcpyAsync(k.d_htab, h.data(), h.size() * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-    PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // h is a local buffer
+    PV_HIP(hipMemcpyAsync(k.d_htab, h, ((size_t)k.hmask + 1) * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+    if (!hbuf) PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // h is a local buffer
     return PV_OK;
 }
 
@@ -1777,7 +1856,12 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
-            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
+#if PV_COMB_A_QUEUE
+            const unsigned agrid = std::min<unsigned>(grid, 4u * (unsigned)std::max(1, g_ctx.cus));
+#else
+            const unsigned agrid = grid;
+#endif
+            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(agrid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_straus_done, 0), PV_ERR_LAUNCH);
         } else {
@@ -1859,6 +1943,7 @@ int pv_init(int device) {
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_verdict_copied, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     std::vector<uint32_t> bt(PV_BTAB_ENTRIES * PV_BTAB_STRIDE);
     pv_build_b_table(bt.data());
     PV_HIP(hipMalloc((void**)&g_ctx.d_btab, bt.size() * 4), PV_ERR_ALLOC);
@@ -1991,13 +2076,15 @@ void pv_shutdown(void) {
     if (g_ctx.sstream) (void)hipStreamDestroy(g_ctx.sstream);
     if (g_ctx.ev_straus_done) (void)hipEventDestroy(g_ctx.ev_straus_done);
     if (g_ctx.ev_launch_done) (void)hipEventDestroy(g_ctx.ev_launch_done);
+    if (g_ctx.ev_verdict_copied) (void)hipEventDestroy(g_ctx.ev_verdict_copied);
+    if (g_ctx.kc.ev_async) (void)hipEventDestroy(g_ctx.kc.ev_async);
     g_ctx = Ctx();
 }
 
 int pv_last_path(int* path, uint32_t* nkeys) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_last_path: call pv_init first");
-    uint32_t u[PV_SPLIT_WORDS] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t u[PV_SPLIT_WORDS] = {};
     if (g_ctx.last_keyed) {
         PV_HIP(hipStreamSynchronize(g_ctx.stream), PV_ERR_LAUNCH);
         PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
@@ -2172,6 +2259,12 @@ static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* s
 // included (profiles/r02/latency_vs_keyed_crossover.txt): 3,072 requests 0.64 vs 0.71 ms, 4,096
 // 0.65 vs 0.92; at 2 requests per key (2,048) the latency path still wins (0.58 vs 0.61). Keys in
 // the node-side key cache make the latency path faster still: no hint while the cache holds keys.
+#ifndef PV_KC_AUTO_MAX_BATCH
+#define PV_KC_AUTO_MAX_BATCH 4096  // automatic admission counts keys of host batches up to this size
+#endif
+static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async);
+static void kc_auto_count(const uint8_t* pk, uint64_t n, std::vector<uint8_t>& admit);
+
 static bool pv_keyed_hint(const uint8_t* pk, uint64_t n) {
     if (g_ctx.path != PV_PATH_AUTO || n < PV_KEYED_HINT_MIN || n > PV_LATENCY_MAX) return false;
     if (g_ctx.kc.enabled && !g_ctx.kc.index.empty()) return false;
@@ -2263,7 +2356,25 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     if (rc) return rc;
     uint64_t* hver = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
     PV_HIP(hipMemcpyAsync(hver, dver, vwords * 8, hipMemcpyDeviceToHost, s), PV_ERR_LAUNCH);
-    PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
+    // automatic key-cache admission: keys seen auto_min times get their tables built right behind
+    // this batch on the same stream; only the verdict copy is waited for, the build overlaps the
+    // caller's next steps (the next launch is ordered after it)
+    auto& k = g_ctx.kc;
+    std::vector<uint8_t> admit;
+    if (k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken && n <= PV_KC_AUTO_MAX_BATCH) kc_auto_count(pk, n, admit);
+    if (!admit.empty()) {
+        PV_HIP(hipEventRecord(g_ctx.ev_verdict_copied, s), PV_ERR_LAUNCH);
+        const std::string err = g_err;
+        if (kc_put_locked(admit.data(), admit.size() / 32, true) == PV_OK) {
+            k.auto_admitted += admit.size() / 32;
+        } else {
+            k.auto_failed += admit.size() / 32;  // the verdicts stand; the keys stay uncached
+            g_err = err;
+        }
+        PV_HIP(hipEventSynchronize(g_ctx.ev_verdict_copied), PV_ERR_LAUNCH);
+    } else {
+        PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
+    }
     memcpy(verdict_bits, hver, (n + 7) / 8);  // little-endian words, LSB-first bits
     return PV_OK;
 }
@@ -2338,10 +2449,14 @@ int pv_key_cache_configure(uint32_t capacity) {
         (e = hipMalloc((void**)&k.d_flags, (uint64_t)capacity * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&k.d_htab, (uint64_t)H * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&k.d_put_pk, (uint64_t)g_ctx.kw.kcap * 32)) != hipSuccess ||
-        (e = hipMalloc((void**)&k.d_put_slot, (uint64_t)g_ctx.kw.kcap * 4)) != hipSuccess) {
+        (e = hipMalloc((void**)&k.d_put_slot, (uint64_t)g_ctx.kw.kcap * 4)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&k.h_async, (uint64_t)g_ctx.kw.kcap * 36 + (uint64_t)H * 4,
+                           hipHostMallocDefault)) != hipSuccess ||
+        (!k.ev_async && (e = hipEventCreateWithFlags(&k.ev_async, hipEventDisableTiming)) != hipSuccess)) {
         kc_free();
         return fail(PV_ERR_ALLOC, std::string("pv_key_cache_configure: hipMalloc: ") + hipGetErrorString(e));
     }
+    k.h_async_cap = (uint64_t)g_ctx.kw.kcap * 36 + (uint64_t)H * 4;
     k.cap = capacity;
     k.hmask = H - 1;
     k.seed = (uint32_t)std::random_device{}() | 1u;
@@ -2351,39 +2466,47 @@ int pv_key_cache_configure(uint32_t capacity) {
 }
 
 // Builds the fresh keys' tables (slot PV_KC_EMPTY = evicted again within the same put) into their
-// cache slots, in batches of the workspace's comb capacity. PV_TEST_FAIL_KC_PUT_BATCH=b (tests
-// only) reports a failure after batch b has been built and scattered, to exercise the rollback.
-static int kc_build_tables(const std::vector<std::string>& fresh, const std::vector<uint32_t>& fresh_slot) {
+// cache slots, in batches of the workspace's comb capacity. async: one batch only (the caller caps
+// the keys), staged through the pinned h_async area and left running on the engine stream (the
+// next launch is stream-ordered after it). PV_TEST_FAIL_KC_PUT_BATCH=b (tests only) reports a
+// failure after batch b has been enqueued, to exercise the rollback.
+static int kc_build_tables(const std::vector<std::string>& fresh, const std::vector<uint32_t>& fresh_slot,
+                           bool async) {
     auto& k = g_ctx.kc;
     hipStream_t s = g_ctx.stream;
     if (g_ctx.last_stream && g_ctx.last_stream != s) PV_HIP(hipStreamWaitEvent(s, g_ctx.ev_launch_done, 0), PV_ERR_LAUNCH);
     const char* fail_env = getenv("PV_TEST_FAIL_KC_PUT_BATCH");
     const long fail_batch = fail_env ? atol(fail_env) : -1;
     KeyWork kw = g_ctx.kw;
-    std::vector<uint32_t> ident(kw.kcap);
-    for (uint32_t j = 0; j < kw.kcap; j++) ident[j] = j;
-    PV_HIP(hipMemcpyAsync(kw.comb_key, ident.data(), (uint64_t)kw.kcap * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-    PV_HIP(hipMemcpyAsync(kw.key_owner, ident.data(), (uint64_t)kw.kcap * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-    std::vector<uint8_t> bpk;
-    std::vector<uint32_t> bslot;
+    std::vector<uint8_t> lpk;
+    std::vector<uint32_t> lslot;
     long batch = 0;
     for (size_t f0 = 0; f0 < fresh.size();) {
-        bpk.clear();
-        bslot.clear();
+        uint8_t* bpk;
+        uint32_t* bslot;
+        if (async) {  // pinned: keys [kcap][32], then slots [kcap]
+            bpk = k.h_async;
+            bslot = reinterpret_cast<uint32_t*>(k.h_async + (uint64_t)kw.kcap * 32);
+        } else {
+            lpk.resize((uint64_t)kw.kcap * 32);
+            lslot.resize(kw.kcap);
+            bpk = lpk.data();
+            bslot = lslot.data();
+        }
+        uint32_t m = 0;
         size_t f = f0;
-        for (; f < fresh.size() && bslot.size() < kw.kcap; f++) {
+        for (; f < fresh.size() && m < kw.kcap; f++) {
             if (fresh_slot[f] == PV_KC_EMPTY) continue;
-            bpk.insert(bpk.end(), fresh[f].begin(), fresh[f].end());
-            bslot.push_back(fresh_slot[f]);
+            memcpy(bpk + 32ull * m, fresh[f].data(), 32);
+            bslot[m++] = fresh_slot[f];
         }
         f0 = f;
-        const uint32_t m = (uint32_t)bslot.size();
         if (m == 0) continue;
-        const uint32_t cnt[PV_SPLIT_WORDS] = {m, m, 0, 0, 0, 0, 0, 0};  // keys, comb keys; sparse, lat = 0
-        PV_HIP(hipMemcpyAsync(k.d_put_pk, bpk.data(), bpk.size(), hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-        PV_HIP(hipMemcpyAsync(k.d_put_slot, bslot.data(), (uint64_t)m * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-        PV_HIP(hipMemcpyAsync(kw.nkeys, cnt, sizeof(cnt), hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-        PV_HIP(hipMemsetAsync(kw.comb_cslot, 0xFF, (uint64_t)m * 4, s), PV_ERR_LAUNCH);  // build every table
+        if (async && f0 < fresh.size()) return fail(PV_ERR_ARG, "kc_build_tables: asynchronous put above one batch");
+        PV_HIP(hipMemcpyAsync(k.d_put_pk, bpk, 32ull * m, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpyAsync(k.d_put_slot, bslot, (uint64_t)m * 4, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        hipLaunchKernelGGL(pv_kc_put_prep_kernel, dim3((m + PV_BLOCK - 1) / PV_BLOCK), dim3(PV_BLOCK), 0, s, kw, m);
+        PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         const Gate gate{kw.nkeys, kw.slot_req};
         hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(m, PV_LP_CHAIN_BLOCKS)), dim3(64), 0, s,
                            k.d_put_pk, kw, gate, 0, PV_COMB_POS);
@@ -2395,18 +2518,20 @@ static int kc_build_tables(const std::vector<std::string>& fresh, const std::vec
         hipLaunchKernelGGL(pv_kc_scatter_kernel, dim3(64, m), dim3(PV_BLOCK), 0, s, kw.ctab, kw.key_flag, k.d_put_pk,
                            k.d_put_slot, m, k.d_tab, k.d_flags, k.d_keys);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-        PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // bpk / bslot / cnt are host locals
+        if (!async) PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // bpk / bslot are host locals
         if (batch++ == fail_batch) return fail(PV_ERR_LAUNCH, "pv_key_cache_put: injected failure (PV_TEST_FAIL_KC_PUT_BATCH)");
     }
     return PV_OK;
 }
 
-int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
-    std::lock_guard<std::mutex> lk(g_mu);
+// pv_key_cache_put under g_mu. async (automatic admission): at most kcap new keys, nothing waited
+// for (pinned staging; the hash-table upload and ev_launch_done are stream-ordered after the build).
+static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async) {
     auto& k = g_ctx.kc;
-    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: call pv_init first");
-    if (k.cap == 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: cache not configured");
-    if (n > 0 && !pks) return fail(PV_ERR_ARG, "pv_key_cache_put: null pointer");
+    if (async) {
+        if (k.async_pending) PV_HIP(hipEventSynchronize(k.ev_async), PV_ERR_LAUNCH);  // h_async is free again
+        k.async_pending = false;
+    }
     // slots for the new keys (at most cap of them: the last cap distinct keys of the call win).
     // The device hash table still holds the state before this call until kc_upload_htab below.
     std::vector<std::string> fresh;
@@ -2436,7 +2561,7 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
         fresh_slot.push_back(slot);
         touched.push_back(slot);
     }
-    int rc = kc_build_tables(fresh, fresh_slot);
+    int rc = kc_build_tables(fresh, fresh_slot, async);
     if (rc != PV_OK) {
         // roll back to a state in which every indexed key's table is built: every slot this call
         // assigned (its new key's table may be unbuilt, and its evicted key's table may already be
@@ -2462,11 +2587,89 @@ int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
         return rc;
     }
     g_ctx.last_keyed = false;
+    if (async) {
+        rc = kc_upload_htab(g_ctx.stream, reinterpret_cast<uint32_t*>(k.h_async + (uint64_t)g_ctx.kw.kcap * 36));
+        if (rc == PV_OK) {
+            PV_HIP(hipEventRecord(k.ev_async, g_ctx.stream), PV_ERR_LAUNCH);
+            k.async_pending = true;
+        }
+    } else {
+        rc = kc_upload_htab(g_ctx.stream);
+    }
     PV_HIP(hipEventRecord(g_ctx.ev_launch_done, g_ctx.stream), PV_ERR_LAUNCH);
     g_ctx.last_stream = g_ctx.stream;
-    rc = kc_upload_htab(g_ctx.stream);
     k.broken = rc != PV_OK;  // a complete upload also repairs an earlier failed one
     return rc;
+}
+
+static constexpr uint32_t PV_KC_SEEN_H = 1u << 16;
+
+// Automatic admission: count this batch's keys; the keys reaching auto_min appearances (and not yet
+// admitted in this window) are returned, at most kcap of them.
+static void kc_auto_count(const uint8_t* pk, uint64_t n, std::vector<uint8_t>& admit) {
+    auto& k = g_ctx.kc;
+    if (k.seen_key.empty()) {
+        k.seen_key.assign((size_t)PV_KC_SEEN_H * 4, 0);
+        k.seen_cnt.assign(PV_KC_SEEN_H, 0);
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t w[4];
+        memcpy(w, pk + 32 * i, 32);
+        if (k.seen_used >= PV_KC_SEEN_H / 2) {  // a new counting window
+            std::fill(k.seen_cnt.begin(), k.seen_cnt.end(), 0);
+            k.seen_used = 0;
+        }
+        uint32_t h = (uint32_t)(((w[0] ^ w[3]) * 0x9E3779B97F4A7C15ull) >> 48) & (PV_KC_SEEN_H - 1);
+        for (;;) {
+            uint8_t& c = k.seen_cnt[h];
+            uint64_t* e = &k.seen_key[(size_t)h * 4];
+            if (c == 0) {  // first appearance in this window
+                memcpy(e, w, 32);
+                c = 1;
+                k.seen_used++;
+                if (k.auto_min <= 1) {
+                    c = 255;
+                    admit.insert(admit.end(), pk + 32 * i, pk + 32 * i + 32);
+                }
+                break;
+            }
+            if (e[0] == w[0] && e[1] == w[1] && e[2] == w[2] && e[3] == w[3]) {
+                if (c != 255 && ++c >= k.auto_min) {
+                    c = 255;
+                    admit.insert(admit.end(), pk + 32 * i, pk + 32 * i + 32);
+                }
+                break;
+            }
+            h = (h + 1) & (PV_KC_SEEN_H - 1);
+        }
+        if (admit.size() >= 32ull * g_ctx.kw.kcap) break;
+    }
+}
+
+int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& k = g_ctx.kc;
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: call pv_init first");
+    if (k.cap == 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_put: cache not configured");
+    if (n > 0 && !pks) return fail(PV_ERR_ARG, "pv_key_cache_put: null pointer");
+    return kc_put_locked(pks, n, false);
+}
+
+int pv_key_cache_auto(uint32_t min_seen) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_auto: call pv_init first");
+    if (min_seen > 254) return fail(PV_ERR_ARG, "pv_key_cache_auto: min_seen above 254");
+    g_ctx.kc.auto_min = min_seen;
+    g_ctx.kc.seen_used = 0;
+    std::fill(g_ctx.kc.seen_cnt.begin(), g_ctx.kc.seen_cnt.end(), 0);
+    return PV_OK;
+}
+
+int pv_key_cache_auto_stats(uint64_t* admitted, uint64_t* failed) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (admitted) *admitted = g_ctx.kc.auto_admitted;
+    if (failed) *failed = g_ctx.kc.auto_failed;
+    return PV_OK;
 }
 
 int pv_key_cache_clear(void) {

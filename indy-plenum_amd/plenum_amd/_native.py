@@ -74,6 +74,8 @@ SIGNATURES = {
     "pv_key_cache_enable": (ctypes.c_int, [ctypes.c_int]),
     "pv_key_cache_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "pv_key_cache_contains": (ctypes.c_int, [ctypes.c_void_p]),
+    "pv_key_cache_auto": (ctypes.c_int, [ctypes.c_uint32]),
+    "pv_key_cache_auto_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "pv_stream_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "pv_stream_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_stream_sync": (ctypes.c_int, [ctypes.c_void_p]),
@@ -262,6 +264,18 @@ class KeyCache:
         size, cap = ctypes.c_uint32(), ctypes.c_uint32()
         check(lib().pv_key_cache_stats(ctypes.byref(size), ctypes.byref(cap)), "pv_key_cache_stats")
         return size.value, cap.value
+
+    @staticmethod
+    def auto(min_seen):
+        """Automatic admission: a key seen min_seen times in host batches of <= 4,096 requests is put
+        into the cache behind that batch (0 = off)."""
+        check(lib().pv_key_cache_auto(int(min_seen)), "pv_key_cache_auto")
+
+    @staticmethod
+    def auto_stats():
+        a, f = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().pv_key_cache_auto_stats(ctypes.byref(a), ctypes.byref(f)), "pv_key_cache_auto_stats")
+        return a.value, f.value
 
     @staticmethod
     def contains(pk):

@@ -185,3 +185,41 @@ def test_put_failure_rolls_back(nat, sodium, oracle, monkeypatch):
     nat.set_path(nat.PV_PATH_AUTO)
     with pytest.raises(ValueError):
         kc.contains(keys[0][:31])
+
+
+def test_automatic_admission(nat, sodium, oracle, monkeypatch):
+    """pv_key_cache_auto(2): a key is put into the cache behind the host batch in which it is seen
+    for the second time (no manual put); verdicts are libsodium's before, during and after the
+    admission (bad keys are admitted with their failing key-check flag), and a failing admission
+    leaves the verdicts unchanged and the keys uncached."""
+    cases, keys, bad = _batch(sodium, oracle, seed=55, n=600)
+    blob, off, pks = pack(cases)
+    want = _want(sodium, cases)
+    kc = nat.KeyCache
+    kc.configure(4096)
+    kc.auto(2)
+    nat.set_path(nat.PV_PATH_AUTO)
+    distinct = {bytes(p) for p in pks}
+    try:
+        a0, _ = kc.auto_stats()
+        assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)  # 1st sighting of every key
+        assert kc.stats()[0] == 0
+        assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)  # 2nd: admitted behind the batch
+        a1, f1 = kc.auto_stats()
+        assert a1 - a0 == len(distinct) and f1 == 0
+        assert kc.stats()[0] == len(distinct) and all(kc.contains(k) for k in keys)
+        for _ in range(2):  # now verified from the cached tables
+            assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+        # a failing admission: verdicts stand, nothing new is cached
+        kc.clear()
+        kc.auto(2)  # a new counting window
+        monkeypatch.setenv("PV_TEST_FAIL_KC_PUT_BATCH", "0")
+        assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+        assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+        monkeypatch.delenv("PV_TEST_FAIL_KC_PUT_BATCH")
+        a2, f2 = kc.auto_stats()
+        assert a2 == a1 and f2 == len(distinct) and kc.stats()[0] == 0
+        assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+    finally:
+        kc.auto(0)
+        kc.configure(0)
