@@ -42,7 +42,7 @@ from collections import namedtuple
 
 from .constants import IDENTIFIER, OPERATION, REQ_ID, SIGNATURES
 from .exceptions import BaseExc, InvalidClientMsgType, InvalidClientRequest
-from .node_messages import CLIENT_OPS, OP_FIELD_NAME, MessageFactory, NodeMessageType, validate_node_message
+from .node_messages import CLIENT_OPS, OP_FIELD_NAME, MessageFactory, NodeMessageType, validate_node_message  # noqa: F401
 from .wire import Request
 
 PROPAGATE = "PROPAGATE"       # plenum/common/constants.py PROPAGATE
