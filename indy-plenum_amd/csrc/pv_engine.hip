@@ -264,8 +264,7 @@ static constexpr int PV_SPLIT_COMB_KEYS = 1;   // keys given a comb table
 static constexpr int PV_SPLIT_SLOTS = 2;       // requests (slots) of those keys
 static constexpr int PV_SPLIT_SPARSE = 3;      // 1: the comb tables are filled sparsely (small chunk)
 static constexpr int PV_SPLIT_LAT = 4;         // 1: the dedup chose the latency path for this chunk
-static constexpr int PV_SPLIT_QUEUE = 8;       // [8..15]: pv_comb_a_kernel's per-XCD tile counters
-static constexpr uint32_t PV_SPLIT_WORDS = 16; // counters cleared per keyed chunk
+static constexpr uint32_t PV_SPLIT_WORDS = 8;  // counters cleared per keyed chunk
 struct Gate {
     const uint32_t* split;
     const uint32_t* slot_req;
@@ -1372,45 +1371,14 @@ __device__ __forceinline__ void pv_comb_a_slot(const Work& wk, const KeyWork& kw
     }
 }
 
-// Tile scheduling of pv_comb_a_kernel. PV_COMB_A_QUEUE = 1: a resident grid (4 workgroups per CU)
-// takes 256-slot tiles from per-XCD work queues (atomic counters in nkeys[PV_SPLIT_QUEUE + x]): XCD
-// x owns a contiguous range of the key-sorted tiles (a key's table rows stay in its L2) and, once
-// its range is drained, helps the other XCDs. Nothing is quantised into rounds of the chip's 1,024
-// workgroup slots, so the few slots a split chunk's Straus-side waves hold (config 3) cost only
-// their share of the work instead of a fifth partial round. 0: one workgroup per tile, XCD-remapped.
-#ifndef PV_COMB_A_QUEUE
-#define PV_COMB_A_QUEUE 1
-#endif
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                Gate gate) {
     if (!gate.keyed() || gate.off()) return;
+    const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
+    if (i >= gate.ncomb()) return;
     __shared__ uint4 stg[PV_BLOCK / 64][10][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nc = gate.ncomb();
-#if PV_COMB_A_QUEUE
-    __shared__ uint32_t s_tile;
-    const uint32_t ntiles = (nc + PV_BLOCK - 1) / PV_BLOCK;
-    const uint32_t q = ntiles >> 3, r = ntiles & 7;
-    const uint32_t home = blockIdx.x & 7;  // workgroups are dispatched to the XCDs round-robin
-    for (uint32_t probe = 0; probe < 8; probe++) {
-        const uint32_t x = (home + probe) & 7;
-        const uint32_t lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-        const uint32_t cnt = q + (x < r ? 1u : 0u);
-        for (;;) {
-            __syncthreads();  // every wave is done with s_tile and the staging area
-            if (threadIdx.x == 0) s_tile = atomicAdd(&kw.nkeys[PV_SPLIT_QUEUE + x], 1u);
-            __syncthreads();
-            const uint32_t t = s_tile;
-            if (t >= cnt) break;  // uniform over the workgroup: every wave leaves this range together
-            const uint32_t i = (lo + t) * PV_BLOCK + threadIdx.x;  // slot
-            if (i < nc) pv_comb_a_slot(wk, kw, i, &stg[wv][0][0]);
-        }
-    }
-#else
-    const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
-    if (i >= nc) return;
     pv_comb_a_slot(wk, kw, i, &stg[wv][0][0]);
-#endif
 }
 
 // Kernel 3: encode Q for PV_ENC_BATCH requests per lane with one shared inversion, compare with R,
@@ -1856,12 +1824,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
-#if PV_COMB_A_QUEUE
-            const unsigned agrid = std::min<unsigned>(grid, 4u * (unsigned)std::max(1, g_ctx.cus));
-#else
-            const unsigned agrid = grid;
-#endif
-            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(agrid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
+            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_straus_done, 0), PV_ERR_LAUNCH);
         } else {
