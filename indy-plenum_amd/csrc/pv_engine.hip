@@ -264,8 +264,7 @@ static constexpr int PV_SPLIT_COMB_KEYS = 1;   // keys given a comb table
 static constexpr int PV_SPLIT_SLOTS = 2;       // requests (slots) of those keys
 static constexpr int PV_SPLIT_SPARSE = 3;      // 1: the comb tables are filled sparsely (small chunk)
 static constexpr int PV_SPLIT_LAT = 4;         // 1: the dedup chose the latency path for this chunk
-static constexpr int PV_SPLIT_QUEUE = 8;       // [8..15]: pv_comb_a_kernel's per-XCD tile counters (A/B)
-static constexpr uint32_t PV_SPLIT_WORDS = 16; // counters cleared per keyed chunk
+static constexpr uint32_t PV_SPLIT_WORDS = 8;  // counters cleared per keyed chunk
 struct Gate {
     const uint32_t* split;
     const uint32_t* slot_req;
@@ -1372,41 +1371,14 @@ __device__ __forceinline__ void pv_comb_a_slot(const Work& wk, const KeyWork& kw
     }
 }
 
-// PV_COMB_A_QUEUE (A/B switch, default off): a resident grid whose WAVES take 64-slot tiles from
-// per-XCD atomic counters (nkeys[PV_SPLIT_QUEUE + x]; XCD x owns a contiguous range, then helps the
-// others), so a chunk whose Straus-side waves hold a few slots is not quantised into a fifth round.
-#ifndef PV_COMB_A_QUEUE
-#define PV_COMB_A_QUEUE 0
-#endif
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                Gate gate) {
     if (!gate.keyed() || gate.off()) return;
-    __shared__ uint4 stg[PV_BLOCK / 64][10][64];
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if PV_COMB_A_QUEUE
-    const uint32_t nc = gate.ncomb();
-    const uint32_t ntiles = (nc + 63) / 64;
-    const uint32_t q = ntiles >> 3, r = ntiles & 7;
-    const uint32_t home = blockIdx.x & 7;  // workgroups are dispatched to the XCDs round-robin
-    const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t probe = 0; probe < 8; probe++) {
-        const uint32_t x = (home + probe) & 7;
-        const uint32_t lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-        const uint32_t cnt = q + (x < r ? 1u : 0u);
-        for (;;) {
-            uint32_t t = 0;
-            if (lane == 0) t = atomicAdd(&kw.nkeys[PV_SPLIT_QUEUE + x], 1u);
-            t = __builtin_amdgcn_readfirstlane(t);
-            if (t >= cnt) break;  // wave-uniform
-            const uint32_t i = (lo + t) * 64 + lane;  // slot
-            if (i < nc) pv_comb_a_slot(wk, kw, i, &stg[wv][0][0]);
-        }
-    }
-#else
     const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
+    __shared__ uint4 stg[PV_BLOCK / 64][10][64];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     pv_comb_a_slot(wk, kw, i, &stg[wv][0][0]);
-#endif
 }
 
 // Kernel 3: encode Q for PV_ENC_BATCH requests per lane with one shared inversion, compare with R,
@@ -1852,12 +1824,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
-#if PV_COMB_A_QUEUE
-            const unsigned agrid = std::min<unsigned>(grid, 4u * (unsigned)std::max(1, g_ctx.cus));
-#else
-            const unsigned agrid = grid;
-#endif
-            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(agrid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
+            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_straus_done, 0), PV_ERR_LAUNCH);
         } else {
