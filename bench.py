@@ -822,6 +822,32 @@ def main():
                                "path": _native.last_path()[0], "ok": okk}
             return lat
         lat = latency_at((1, 100, 1000, 4096, 10000, 32768))
+
+        # the device-buffer call at 2,049-4,096 requests: AUTO's latency-vs-keyed choice is made on
+        # the device by the dedup kernels (no host key count); median of 20 enqueue+sync rounds
+        def device_latency_at(sizes):
+            out = {}
+            for k in sizes:
+                ko = off[:k + 1]
+                kb = DeviceBatch(blob[:int(ko[-1])], ko, pks[:k])
+                try:
+                    kb.verify()
+                    _native.check(L.pv_sync(), "pv_sync")
+                    ts = []
+                    for _ in range(20):
+                        t1 = time.perf_counter()
+                        kb.verify()
+                        _native.check(L.pv_sync(), "pv_sync")
+                        ts.append(time.perf_counter() - t1)
+                    okk = bool(np.array_equal(bits(kb.verdict_words(), k), want_local[:k]))
+                    out[str(k)] = {"median_ms": round(1e3 * float(np.median(ts)), 3), "path": _native.last_path()[0],
+                                   "ok": okk}
+                finally:
+                    kb.free()
+            out["note"] = ("pv_verify_batch_device on HBM-resident inputs (no PCIe), AUTO; path 2 = keyed "
+                           "(the dedup counted >= 3 requests per key), 3 = latency")
+            return out
+        lat["device_call"] = device_latency_at((2048, 3072, 4096))
         # automatic admission (pv_key_cache_auto(2)), no manual put: a signer's key is cached behind
         # the second batch it appears in, so the repeat calls of latency_at run on cached tables
         _native.KeyCache.configure(2048)

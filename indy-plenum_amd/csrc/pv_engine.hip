@@ -215,7 +215,17 @@ struct LdsBTab {
 // the Straus loop enters a new group of 8 windows.
 // digits rows: 0..7 k (both paths), 8.. S: 8 packed words (Straus, radix 256) or PV_BC2_POS signed
 // radix-2^W digits (comb path, wide fixed-base comb)
-static constexpr int PV_DIGIT_ROWS = 8 + (PV_BC2_POS > 8 ? PV_BC2_POS : 8);
+// Radix of the wide fixed-base comb chosen at pv_init: PV_BC2_W (24: 10.7 GB of HBM) or, when that
+// allocation fails (or PV_FORCE_BCOMB16 is set), W = 16 over the radix-65536 comb T_B the latency
+// path already holds (the same layout and digits: comb.h). Kernels that recode or read S's digits
+// are instantiated for both.
+template <int W>
+struct Bc2 {
+    static constexpr int POS = (253 + W - 1) / W;
+    static constexpr uint32_t ENT = (1u << (W - 1)) + 1u;
+};
+static_assert(Bc2<16>::ENT == PV_BCOMB_ENT && Bc2<16>::POS == PV_BCOMB_POS, "W = 16 is the radix-65536 comb");
+static constexpr int PV_DIGIT_ROWS = 8 + (Bc2<16>::POS > PV_BC2_POS ? Bc2<16>::POS : PV_BC2_POS);
 struct DevDigits {
     Soa d;
     uint32_t slot;
@@ -352,6 +362,7 @@ static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 
 // Straus path, per slot i (request r): checks, decompression of A, k = SHA-512(R||A||M) mod L,
 // recoding; -A for the table kernel.
+template <int W>
 __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, const uint64_t* __restrict__ off,
                                              const uint8_t* __restrict__ pk, const Work& wk, uint32_t i, uint32_t r) {
     const uint64_t o0 = off[r], o1 = off[r + 1];
@@ -389,10 +400,10 @@ __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, con
 #pragma unroll
     for (int q = 0; q < 8; q++) ds.st(q, (uint32_t)i, ek[q]);
 #if PV_STRAUS_WIDE_B
-    int32_t fb[PV_BC2_POS];  // [S]B from the wide fixed-base comb (pv_straus_b_kernel)
-    sc_recode_w<PV_BC2_W, PV_BC2_POS>(fb, in.S);
+    int32_t fb[Bc2<W>::POS];  // [S]B from the wide fixed-base comb (pv_straus_b_kernel)
+    sc_recode_w<W, Bc2<W>::POS>(fb, in.S);
 #pragma unroll
-    for (int j = 0; j < PV_BC2_POS; j++) ds.st(8 + j, (uint32_t)i, (uint32_t)fb[j]);
+    for (int j = 0; j < Bc2<W>::POS; j++) ds.st(8 + j, (uint32_t)i, (uint32_t)fb[j]);
 #else
     uint32_t fs[8];
     sc_recode256(fs, in.S);
@@ -416,6 +427,7 @@ __device__ __forceinline__ void pv_straus_prio() {
 }
 
 // Kernel 1 (Straus path): pv_prep_slot over the Straus slots.
+template <int W>
 __global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(const uint8_t* __restrict__ sm,
                                                                const uint64_t* __restrict__ off, uint64_t n,
                                                                const uint8_t* __restrict__ pk, Work wk, Gate gate) {
@@ -426,7 +438,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(co
         const uint32_t sb = gate.stile(t, ntiles);
         if ((sb + 1) * PV_BLOCK <= nc) break;  // this and every later tile: comb-path slots
         const uint32_t i = sb * PV_BLOCK + threadIdx.x;  // slot
-        if (i < n && i >= nc) pv_prep_slot(sm, off, pk, wk, i, gate.req(i));
+        if (i < n && i >= nc) pv_prep_slot<W>(sm, off, pk, wk, i, gate.req(i));
     }
 }
 
@@ -1154,6 +1166,7 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_kc_put_prep_kernel(KeyWork kw, ui
 }
 
 // Per request on the comb path: signature checks, k, key id and validity, radix-256 digits of k, S.
+template <int W>
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t* __restrict__ sm,
                                                                     const uint64_t* __restrict__ off, uint64_t n,
                                                                     const uint8_t* __restrict__ pk, Work wk,
@@ -1179,14 +1192,14 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
     // the key's own checks (key_flag) are written by the chain kernel on the key stream, which
     // runs concurrently with this kernel: pv_comb_a_kernel folds them into flags[slot]
     uint32_t ek[8];
-    int32_t fb[PV_BC2_POS];
+    int32_t fb[Bc2<W>::POS];
     sc_recode256(ek, k);
-    sc_recode_w<PV_BC2_W, PV_BC2_POS>(fb, in.S);
+    sc_recode_w<W, Bc2<W>::POS>(fb, in.S);
     const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
 #pragma unroll
     for (int q = 0; q < 8; q++) ds.st(q, i, ek[q]);
 #pragma unroll
-    for (int j = 0; j < PV_BC2_POS; j++) ds.st(8 + j, i, (uint32_t)fb[j]);
+    for (int j = 0; j < Bc2<W>::POS; j++) ds.st(8 + j, i, (uint32_t)fb[j]);
     wk.flags[i] = ok ? 1u : 0u;
     if (kw.nkeys[PV_SPLIT_SPARSE]) {  // small chunk: record which entries of each row this request uses
         uint32_t* nd = kw.need + (uint64_t)kw.skey[i] * PV_COMB_POS * 5;
@@ -1201,12 +1214,13 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
 
 // Wide fixed-base comb rows (comb.h PV_BC2_*): row j = entries 0..PV_BC2_ENT-1 of [d 2^(W j)] B,
 // 8 uint4 each, LDS-staged like DevBStage; 64-bit entry index (the table is ~10.7 GB at W = 24).
+template <uint32_t ENT>
 struct DevB2Stage {
     const uint4* base;
     uint4* lds;
     uint32_t lane;
     __device__ __forceinline__ void stage(int j, int d) const {
-        const uint4* e = base + ((uint64_t)j * PV_BC2_ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4);
+        const uint4* e = base + ((uint64_t)j * ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4);
         pv_lds_reads_done();
         pv_glds16_row<PV_BCOMB_STRIDE / 4>(e, lds);
     }
@@ -1227,6 +1241,7 @@ struct DevB2Stage {
 // positions: one entry conversion + PV_BC2_POS - 1 additions). Needs no per-key data, so it runs on
 // the main stream while the key stream builds the tables. acc (extended, 40 words) goes to q rows
 // 0..39.
+template <int W>
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
                                                                  Gate gate) {
     if (!gate.keyed() || gate.off()) return;
@@ -1236,8 +1251,8 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
     ge_p3 acc;
     __shared__ uint4 stg[PV_BLOCK / 64][PV_BCOMB_STRIDE / 4][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    pv_comb_b_acc_w<PV_BC2_POS>(acc, DevB2Stage{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
-                                [&](int j) { return dig.fb(j); });
+    pv_comb_b_acc_w<Bc2<W>::POS>(acc, DevB2Stage<Bc2<W>::ENT>{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
+                                 [&](int j) { return dig.fb(j); });
     const Soa qs(wk.q, 40, wk.stride);
 #pragma unroll
     for (int q = 0; q < 10; q++) {
@@ -1250,6 +1265,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
 
 // Straus path, [S]B of every Straus slot from the wide fixed-base comb (tiles from the end of the
 // slot range, like the other Straus kernels), extended, to q rows 0..39 for pv_msm_kernel.
+template <int W>
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_straus_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
                                                                    Gate gate) {
     if (gate.off()) return;
@@ -1267,8 +1283,8 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_straus_b_kernel(uint64_t n, Wo
         const uint32_t i = active ? i0 : (uint32_t)n - 1;  // whole waves stay in step for the staging
         const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
         ge_p3 acc;
-        pv_comb_b_acc_w<PV_BC2_POS>(acc, DevB2Stage{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
-                                    [&](int j) { return dig.fb(j); });
+        pv_comb_b_acc_w<Bc2<W>::POS>(acc, DevB2Stage<Bc2<W>::ENT>{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
+                                     [&](int j) { return dig.fb(j); });
         if (active) {
 #pragma unroll
             for (int q = 0; q < 10; q++) {
@@ -1484,6 +1500,7 @@ struct Ctx {
     uint32_t last_split[3] = {0, 0, 0};  // PV_SPLIT_* of it, read back by pv_last_path
     uint4* d_bcomb = nullptr;  // fixed-base comb T_B (radix 65536; latency path)
     uint4* d_bc2 = nullptr;    // wide fixed-base comb T_B2 (radix 2^W; comb path's [S]B)
+    int bc2_w = PV_BC2_W;      // its radix: PV_BC2_W, or 16 when d_bc2 aliases d_bcomb (fallback)
     int path = PV_PATH_AUTO;
     // host-entry staging
     uint8_t* h_stage = nullptr;  // pinned
@@ -1628,6 +1645,13 @@ int ensure_events(int count) {
 
 int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk, uint64_t* d_verdict,
                   hipStream_t stream);
+
+// A kernel instantiated per wide-comb radix (Bc2<W>), launched for the radix pv_init chose.
+#define PV_LAUNCH_BC2(k, ...)                                                                      \
+    do {                                                                                           \
+        if (g_ctx.bc2_w == 16) hipLaunchKernelGGL(k<16>, __VA_ARGS__);                             \
+        else hipLaunchKernelGGL(k<PV_BC2_W>, __VA_ARGS__);                                          \
+    } while (0)
 
 // One batch on `stream` (caller holds g_mu). Chunks of at most work.stride requests (a multiple of
 // 64, so verdict words never straddle).
@@ -1792,13 +1816,13 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                 grid, std::max(1u, (unsigned)(PV_SIDE_GRID_PER_CU * std::max(1, g_ctx.cus))));
             PV_HIP(hipStreamWaitEvent(ss, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
 #ifndef PV_AB_NO_SIDE  // measurement-only switch: drops the Straus side (wrong verdicts if it has work)
-            hipLaunchKernelGGL(pv_prep_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
+            PV_LAUNCH_BC2(pv_prep_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_table_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #if PV_STRAUS_WIDE_B
-            hipLaunchKernelGGL(pv_straus_b_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, g_ctx.d_bc2, gate);
+            PV_LAUNCH_BC2(pv_straus_b_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, g_ctx.d_bc2, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #endif
             hipLaunchKernelGGL(pv_msm_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
@@ -1806,7 +1830,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #endif
             PV_HIP(hipEventRecord(g_ctx.ev_straus_done, ss), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+            PV_LAUNCH_BC2(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             // a small chunk's sparse table fill (needs the chain's bases and the need masks comb_prep
@@ -1819,7 +1843,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             // [S]B while the key stream finishes the tables, then join
-            hipLaunchKernelGGL(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
+            PV_LAUNCH_BC2(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
                                gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
@@ -1828,14 +1852,14 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_straus_done, 0), PV_ERR_LAUNCH);
         } else {
-            hipLaunchKernelGGL(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+            PV_LAUNCH_BC2(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #if PV_STRAUS_WIDE_B
-            hipLaunchKernelGGL(pv_straus_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
+            PV_LAUNCH_BC2(pv_straus_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
                                gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #endif
@@ -1960,11 +1984,18 @@ int pv_init(int device) {
         // the wide fixed-base comb, built on the device row by row (one scratch row of Z products)
         {
             const uint64_t rows_ent = (uint64_t)(PV_BC2_POS - 1) * PV_BC2_ENT + PV_BC2_TOP_ENT;
-            if (hipMalloc((void**)&g_ctx.d_bc2, rows_ent * PV_BCOMB_STRIDE * 4) != hipSuccess)
-                return fail(PV_ERR_ALLOC, "pv_init: cannot allocate the wide fixed-base comb (" +
-                                              std::to_string(rows_ent * PV_BCOMB_STRIDE * 4 >> 20) +
-                                              " MiB of HBM at radix 2^" + std::to_string(PV_BC2_W) +
-                                              "); rebuild with EXTRA=-DPV_BCOMB_W=20 (805 MiB) or 16 (67 MiB)");
+            // not enough HBM for the wide table (a smaller part, several processes on one GPU) or
+            // PV_FORCE_BCOMB16 set: [S]B from the radix-65536 comb T_B instead (16 lookups instead of
+            // 11, same verdicts; profiles/r02/ab_bcomb_radix.txt: ~2 % slower per step)
+            const char* force16 = getenv("PV_FORCE_BCOMB16");
+            if (PV_BC2_W == 16 || (force16 && *force16 && *force16 != '0') ||
+                hipMalloc((void**)&g_ctx.d_bc2, rows_ent * PV_BCOMB_STRIDE * 4) != hipSuccess) {
+                (void)hipGetLastError();  // clear a failed allocation's sticky error
+                g_ctx.d_bc2 = g_ctx.d_bcomb;
+                g_ctx.bc2_w = 16;
+            }
+        }
+        if (g_ctx.bc2_w != 16) {
             uint32_t* scratch = nullptr;
             PV_HIP(hipMalloc((void**)&scratch, (uint64_t)PV_BC2_ENT * 40), PV_ERR_ALLOC);
             ge_p3 negB, P;
@@ -2022,7 +2053,8 @@ void pv_shutdown(void) {
                     (void*)g_ctx.kw.req_rank, (void*)g_ctx.kw.nkeys,
                     (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_cid, (void*)g_ctx.kw.comb_key,
                     (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
-                    (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb, (void*)g_ctx.d_bc2, (void*)g_ctx.kw.key_count,
+                    (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb,
+                    (void*)(g_ctx.d_bc2 != g_ctx.d_bcomb ? g_ctx.d_bc2 : nullptr), (void*)g_ctx.kw.key_count,
                     (void*)g_ctx.kw.key_cursor, (void*)g_ctx.kw.slot_req, (void*)g_ctx.kw.req_pos,
                     (void*)g_ctx.kw.skey, (void*)g_ctx.kw.sverdict, (void*)g_ctx.kw.key_cslot,
                     (void*)g_ctx.kw.comb_cslot, (void*)g_ctx.kw.need})

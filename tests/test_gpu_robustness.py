@@ -201,3 +201,44 @@ def test_two_threads_host_and_ingress(nat, sodium, oracle):
     for t in ts:
         t.join(timeout=120)
     assert not errors, errors
+
+
+_BCOMB16_SCRIPT = r"""
+import json, os, sys
+root = sys.argv[1]
+sys.path[:0] = [root, os.path.join(root, "indy-plenum_amd"), os.path.join(root, "tests"), os.path.join(root, "tools")]
+import numpy as np
+import nym_workload, adversarial_batch
+from oracle.oracle import cpu_verdicts
+from plenum_amd import _native
+blob, off, pks = nym_workload.generate(0, 300000, workers=8)
+blob, pks, idx, labels = adversarial_batch.inject(blob, off, pks, 0.02, seed=9)
+want = cpu_verdicts(blob, off, pks)
+_native.ensure_device(0)
+out = {}
+for name in ("auto", "comb", "straus"):
+    _native.set_path(getattr(_native, "PV_PATH_" + name.upper()))
+    got = _native.verify_sm_batch(blob, off, pks)
+    out[name] = {"mismatches": int((got != want).sum()), "split": list(_native.last_split())}
+out["rejected"] = int((~want).sum())
+print(json.dumps(out))
+"""
+
+
+def test_wide_comb_fallback_radix16_bit_exact(sodium):
+    """pv_init's fallback when the 10.7 GB wide fixed-base comb cannot be allocated (forced here with
+    PV_FORCE_BCOMB16): [S]B from the radix-65536 comb on the keyed and Straus paths. A fresh process
+    (the radix is chosen once per pv_init) verifies 300k NYM requests with 2 % adversarial records on
+    every throughput path; verdicts must equal libsodium's."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PV_FORCE_BCOMB16="1")
+    p = subprocess.run([sys.executable, "-c", _BCOMB16_SCRIPT, root], env=env, capture_output=True, text=True,
+                       timeout=170)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert res["rejected"] > 5000
+    for name in ("auto", "comb", "straus"):
+        assert res[name]["mismatches"] == 0, (name, res)
+    assert res["auto"]["split"][1] >= 1024  # the signers took the comb path

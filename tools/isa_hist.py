@@ -16,7 +16,8 @@ VOP2_FAST = {"v_add_u32_e32", "v_sub_u32_e32", "v_and_b32_e32", "v_or_b32_e32", 
 
 
 def kernel_body(text, name):
-    m = re.search(r"^(_Z\d+%s\w*):[^\n]*\n(.*?)^\s*s_endpgm" % re.escape(name), text, re.M | re.S)
+    # the whole function (a gated kernel has an early s_endpgm before its body)
+    m = re.search(r"^(_Z\d+%s\w*):[^\n]*\n(.*?)^\.Lfunc_end" % re.escape(name), text, re.M | re.S)
     if not m:
         raise SystemExit("kernel %s not found" % name)
     return m.group(1), [l.strip() for l in m.group(2).split("\n")]
