@@ -44,6 +44,15 @@ MAC_PER_VERIFY = MAC_DECOMPRESS + MAC_TABLE + MAC_LOOP + MAC_ENCODE
 # algorithmic work is libsodium's loop without the B-scalar half of the sliding-window additions:
 # 253 doublings + 42.7 additions; the encoding runs in pv_encode_kernel.
 MAC_MSM_KERNEL = _mac(_S_LOOP, 253 * 3 + _ADDS / 2 * 8)
+# The built Straus kernel runs the half-size form of the same check (indy-plenum_amd/csrc/sc25519.h
+# sc_halfsize): k = k1 / k2 (mod 8L) with |k1|, k2 < 2^128, so Q' = [k1](+-A) + [k2](-R') over 32
+# regular radix-16 windows of both scalars -- 31 x 4 doublings (4 S + 3 M; the last of each window to
+# extended, +1 M), per window one cached addition to extended (4 M + 4 M) and one to projective (4 M +
+# 3 M) -- then + [k2 S]B (1 M cached form + 4 M + 4 M) and + R' (4 M + 3 M; +1 M for the window's
+# output to extended). Its roofline uses this count (the wave-uniform window count actually executed,
+# ~33.9 on average at random scalars, is inefficiency against it). A different algorithm than
+# MAC_MSM_KERNEL's, counted the same way.
+MAC_MSM_HALF_KERNEL = _mac(124 * 4, 124 * 3 + 31 + 32 * 15 + 17)
 
 # The keyed comb path (indy-plenum_amd/csrc/comb.h) performs a DIFFERENT algorithm for the same
 # verdict: per request 32 cached-form additions of radix-256 T_A entries (4 M + 4 M to extended) and

@@ -542,6 +542,18 @@ LP_FN lu lp_straus_a(const LpLane& c, const Digit& digit, const Load& load) {
     return acc;
 }
 
+// [e](P) over the first nw signed radix-16 windows (nw wave-uniform: the half-size split's window
+// count, sc25519.h sc_halfsize; 64 for a full scalar): (nw - 1) x 4 doublings + nw table additions.
+template <class Digit, class Load>
+LP_FN lu lp_straus_nw(const LpLane& c, int nw, const Digit& digit, const Load& load) {
+    lu acc = lp_add_cached(c, lp_identity_ext(c), load(digit(nw - 1)));
+    for (int win = nw - 2; win >= 0; win--) {
+        acc = lp_dbl(c, lp_dbl(c, lp_dbl(c, lp_dbl(c, acc))));
+        acc = lp_add_cached(c, acc, load(digit(win)));
+    }
+    return acc;
+}
+
 // Entry d = |f| of position j of the fixed-base comb T_B (comb.h: affine niels, words y+x at 0..9,
 // y-x at 10..19, 2dxy at 20..29 of a PV_BCOMB_STRIDE-word entry) in lp cached layout
 // [y-x, y+x, 2dxy, 2], negated for f < 0 (y+x <-> y-x, -2dxy).

@@ -45,7 +45,9 @@ static constexpr int PV_BLOCK = 256;
 #define PV_FILL_MINBLOCKS 2
 #endif
 #ifndef PV_MSM_MINBLOCKS
-#define PV_MSM_MINBLOCKS 2  // workgroups per CU the msm kernel's register budget is sized for
+// workgroups per CU the msm kernel's register budget is sized for (3: <= 168 VGPRs, 3 waves/SIMD; the
+// full-length loop fits that at 2 as well)
+#define PV_MSM_MINBLOCKS 3
 #endif
 #ifndef PV_PREP_MINBLOCKS
 #define PV_PREP_MINBLOCKS 2  // Straus prep (decompression + SHA-512 + recoding)
@@ -147,20 +149,52 @@ struct Soa {
 #ifndef PV_ATAB_AOS
 #define PV_ATAB_AOS 1
 #endif
+// Half-size Straus path (sc25519.h sc_halfsize, verify_core.h pv_straus_ar_xyz): k = k1 / k2 (mod 8L)
+// with |k1|, k2 ~ 2^128, so the per-request loop runs ~33 windows of both scalars against two tables
+// ([j](+-A) and [j](-R')) instead of 64 windows of k against one. 0: the full-length loop over k.
+#ifndef PV_STRAUS_HALF
+#define PV_STRAUS_HALF 1
+#endif
+static constexpr uint32_t PV_ATAB_ENT = PV_STRAUS_HALF ? 18u : 9u;  // table entries per slot
 struct DevATab {
     uint4* base;
     uint32_t nslots;
     uint32_t slot;
+    uint32_t t0 = 0;  // first entry of this table in the slot (the R table starts at 9)
     __device__ __forceinline__ uint4& at(int j, int q) const {
 #if PV_ATAB_AOS
-        return base[(slot * 9u + (uint32_t)j) * 10u + (uint32_t)q];
+        // [slot / 64][entry][slot % 64][quad]: a lane's entry is 160 contiguous bytes, and one wave's
+        // ten stores of an entry cover 10 KB contiguously (full lines reach HBM)
+        return base[(((slot >> 6) * PV_ATAB_ENT + t0 + (uint32_t)j) * 64u + (slot & 63u)) * 10u + (uint32_t)q];
 #else
-        return base[(uint32_t)(j * 10 + q) * nslots + slot];
+        return base[(uint32_t)((t0 + j) * 10 + q) * nslots + slot];
 #endif
     }
     __device__ __forceinline__ void store(int j, const uint32_t w[40]) const {
 #pragma unroll
         for (int q = 0; q < 10; q++) at(j, q) = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+    __device__ __forceinline__ void store_p3(int j, const ge_p3& p) const {
+        uint32_t w[40];
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            w[q] = p.X.v[q];
+            w[10 + q] = p.Y.v[q];
+            w[20 + q] = p.Z.v[q];
+            w[30 + q] = p.T.v[q];
+        }
+        store(j, w);
+    }
+    __device__ __forceinline__ void load_p3(int j, ge_p3& p) const {
+        uint32_t w[40];
+        load(j, w);
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            p.X.v[q] = w[q];
+            p.Y.v[q] = w[10 + q];
+            p.Z.v[q] = w[20 + q];
+            p.T.v[q] = w[30 + q];
+        }
     }
     __device__ __forceinline__ void load_half(int j, int h, uint32_t w[20]) const {
 #pragma unroll
@@ -225,13 +259,18 @@ struct Bc2 {
     static constexpr uint32_t ENT = (1u << (W - 1)) + 1u;
 };
 static_assert(Bc2<16>::ENT == PV_BCOMB_ENT && Bc2<16>::POS == PV_BCOMB_POS, "W = 16 is the radix-65536 comb");
-static constexpr int PV_DIGIT_ROWS = 8 + (Bc2<16>::POS > PV_BC2_POS ? Bc2<16>::POS : PV_BC2_POS);
+// half-size Straus path: rows PV_K2_ROW.. hold k2's radix-16 digits, row PV_NW_ROW the lane's window count
+static constexpr int PV_K2_ROW = 8 + (Bc2<16>::POS > PV_BC2_POS ? Bc2<16>::POS : PV_BC2_POS);
+static constexpr int PV_NW_ROW = PV_K2_ROW + 8;
+static constexpr int PV_DIGIT_ROWS = PV_STRAUS_HALF ? PV_NW_ROW + 1 : PV_K2_ROW;
 struct DevDigits {
     Soa d;
     uint32_t slot;
     __device__ __forceinline__ DevDigits(uint32_t* base, uint32_t stride, uint32_t slot_)
         : d(base, PV_DIGIT_ROWS, stride), slot(slot_) {}
     __device__ __forceinline__ uint32_t ek(int q) const { return d.ld(q, slot); }
+    __device__ __forceinline__ uint32_t ek2(int q) const { return d.ld(PV_K2_ROW + q, slot); }
+    __device__ __forceinline__ uint32_t nw() const { return d.ld(PV_NW_ROW, slot); }
     __device__ __forceinline__ uint32_t fs(int q) const { return d.ld(8 + q, slot); }
     __device__ __forceinline__ int fb(int j) const { return (int)d.ld(8 + j, slot); }
 };
@@ -359,6 +398,14 @@ static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 #ifndef PV_STRAUS_WIDE_B
 #define PV_STRAUS_WIDE_B 1
 #endif
+static_assert(!PV_STRAUS_HALF || PV_STRAUS_WIDE_B, "the half-size path takes [k2 S]B from pv_straus_b_kernel");
+
+__device__ __forceinline__ void pv_load_pk(uint32_t A[8], const uint8_t* pk, uint32_t i) {
+    const uint4* p4 = reinterpret_cast<const uint4*>(pk + 32 * (uint64_t)i);
+    const uint4 a0 = p4[0], a1 = p4[1];
+    A[0] = a0.x; A[1] = a0.y; A[2] = a0.z; A[3] = a0.w;
+    A[4] = a1.x; A[5] = a1.y; A[6] = a1.z; A[7] = a1.w;
+}
 
 // Straus path, per slot i (request r): checks, decompression of A, k = SHA-512(R||A||M) mod L,
 // recoding; -A for the table kernel.
@@ -379,6 +426,48 @@ __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, con
     const uint4 a0 = pk4[0], a1 = pk4[1];
     in.A[0] = a0.x; in.A[1] = a0.y; in.A[2] = a0.z; in.A[3] = a0.w;
     in.A[4] = a1.x; in.A[5] = a1.y; in.A[6] = a1.z; in.A[7] = a1.w;
+#if PV_STRAUS_HALF
+    {
+        // pv_prepare_half split over two kernels: here the signature checks, k, its split, digits of
+        // |k1| (rows 0..7) and k2 (PV_K2_ROW..), the window count (row PV_NW_ROW), digits of k2 S mod L,
+        // then A's checks and +-A; R's checks and -R' run in pv_table_kernel
+        bool ok = pv_sig_ok(in, smlen);
+        bool neg;
+        {
+            uint32_t k[8];
+            pv_hash_k(k, in, smlen, mw);
+            pv_halfk hk;
+            sc_halfsize(hk, k);
+            neg = hk.neg;
+            uint32_t s2[8];
+            sc_mul(s2, hk.k2, in.S);
+            const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
+            int32_t fb[Bc2<W>::POS];
+            sc_recode_w<W, Bc2<W>::POS>(fb, s2);
+#pragma unroll
+            for (int j = 0; j < Bc2<W>::POS; j++) ds.st(8 + j, (uint32_t)i, (uint32_t)fb[j]);
+            uint32_t e1[8], e2[8];
+            sc_recode16(e1, hk.k1);
+            sc_recode16(e2, hk.k2);
+            const int nw1 = sc_nwin16(e1), nw2 = sc_nwin16(e2);
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                ds.st(q, (uint32_t)i, e1[q]);
+                ds.st(PV_K2_ROW + q, (uint32_t)i, e2[q]);
+            }
+            ds.st(PV_NW_ROW, (uint32_t)i, (uint32_t)(nw1 > nw2 ? nw1 : nw2));
+        }
+        {
+            ge_p3 PA;  // +-A (k1's sign) to table entry 1 for pv_table_kernel
+            ok &= pv_key_ok_negate(PA, in.A);
+            ge_p3_cneg(PA, neg);
+            const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
+            at.store_p3(1, PA);
+        }
+        wk.flags[i] = ok ? 1u : 0u;
+        return;
+    }
+#endif
 
     ge_p3 negA;
     uint32_t k[8];
@@ -442,8 +531,11 @@ __global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(co
     }
 }
 
-// Kernel 1b: expand -A (extended, in slot 1) into the cached table [j](-A), j = 0..8.
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work wk, Gate gate) {
+// Kernel 1b: the cached table [j](-A), j = 0..8 (full-length path: -A from entry 1); half-size path:
+// decompression and checks of A and R, tables [j](+-A) (entries 0..8) and [j](-R') (entries 9..17).
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(const uint8_t* __restrict__ sm,
+                                                                const uint64_t* __restrict__ off, uint64_t n,
+                                                                const uint8_t* __restrict__ pk, Work wk, Gate gate) {
     if (gate.off()) return;
     pv_straus_prio();
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
@@ -452,6 +544,29 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work 
         if ((sb + 1) * PV_BLOCK <= nc) break;
         const uint32_t i = sb * PV_BLOCK + threadIdx.x;  // slot
         if (i >= n || i < nc) continue;
+#if PV_STRAUS_HALF
+        // [j](+-A) from entry 1 (pv_prep_kernel), then R's canonical-decoding rule and [j](-R')
+        const uint32_t r = gate.req(i);
+        const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[r]);
+        const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+        {
+            DevATab at{wk.atab, (uint32_t)wk.stride, i};
+            ge_p3 PA;
+            at.load_p3(1, PA);
+            pv_build_a_table(at, PA);
+        }
+        bool ok;
+        {
+            uint32_t R[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) R[q] = mw.dw(q);
+            ge_p3 negR;
+            ok = pv_r_decode_negate(negR, R);
+            DevATab rt{wk.atab, (uint32_t)wk.stride, i, 9u};
+            pv_build_a_table(rt, negR);
+        }
+        if (!ok) wk.flags[i] = 0u;
+#else
         const DevATab at{wk.atab, (uint32_t)wk.stride, i};
         uint32_t w[40];
         at.load(1, w);
@@ -464,6 +579,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(uint64_t n, Work 
             negA.T.v[q] = w[30 + q];
         }
         pv_build_a_table(at, negA);
+#endif
     }
 }
 
@@ -494,7 +610,23 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
         const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
         const Soa qs(wk.q, 40, wk.stride);
         fe X, Y, Z;
-#if PV_STRAUS_WIDE_B
+#if PV_STRAUS_HALF
+        // the wave's window count: its lanes' maximum (a lane's digits above its own count are 0)
+        int nw = (int)dig.nw();
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) nw = max(nw, __shfl_xor(nw, m));
+        nw = __builtin_amdgcn_readfirstlane(nw);
+        const DevATab rt{wk.atab, (uint32_t)wk.stride, i, 9u};
+        pv_straus_ar_xyz(X, Y, Z, at, rt, dig, nw, [&](ge_p3& accB) {  // [k2 S]B (pv_straus_b_kernel)
+#pragma unroll
+            for (int q = 0; q < 10; q++) {
+                accB.X.v[q] = qs.ld(q, i);
+                accB.Y.v[q] = qs.ld(10 + q, i);
+                accB.Z.v[q] = qs.ld(20 + q, i);
+                accB.T.v[q] = qs.ld(30 + q, i);
+            }
+        });
+#elif PV_STRAUS_WIDE_B
         pv_straus_a_xyz(X, Y, Z, at, dig, [&](ge_p3& accB) {  // [S]B, written by pv_straus_b_kernel
 #pragma unroll
             for (int q = 0; q < 10; q++) {
@@ -520,12 +652,6 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
 
 // ------------------------------------------------------------------ keyed comb path (comb.h)
 
-__device__ __forceinline__ void pv_load_pk(uint32_t A[8], const uint8_t* pk, uint32_t i) {
-    const uint4* p4 = reinterpret_cast<const uint4*>(pk + 32 * (uint64_t)i);
-    const uint4 a0 = p4[0], a1 = p4[1];
-    A[0] = a0.x; A[1] = a0.y; A[2] = a0.z; A[3] = a0.w;
-    A[4] = a1.x; A[5] = a1.y; A[6] = a1.z; A[7] = a1.w;
-}
 
 __device__ __forceinline__ uint32_t pv_key_hash(const uint32_t A[8], uint32_t seed) {
     uint32_t h = seed;
@@ -1819,7 +1945,8 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_LAUNCH_BC2(pv_prep_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_table_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, gate);
+            hipLaunchKernelGGL(pv_table_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m, d_pk + 32 * c0,
+                               g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #if PV_STRAUS_WIDE_B
             PV_LAUNCH_BC2(pv_straus_b_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, g_ctx.d_bc2, gate);
@@ -1856,7 +1983,8 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                                d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
-            hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, gate);
+            hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m, d_pk + 32 * c0,
+                               g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #if PV_STRAUS_WIDE_B
             PV_LAUNCH_BC2(pv_straus_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
@@ -1937,7 +2065,7 @@ int pv_init(int device) {
     PV_HIP(hipMemcpy(g_ctx.d_btab, bt.data(), bt.size() * 4, hipMemcpyHostToDevice), PV_ERR_ALLOC);
     const uint64_t S = PV_CHUNK;
     g_ctx.work.stride = S;
-    PV_HIP(hipMalloc((void**)&g_ctx.work.atab, S * 9 * 160), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&g_ctx.work.atab, S * PV_ATAB_ENT * 160), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * PV_DIGIT_ROWS * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 40 * 4), PV_ERR_ALLOC);

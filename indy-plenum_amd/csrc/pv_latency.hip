@@ -4,18 +4,23 @@
 // (stp_core/crypto/nacl_wrappers.py:108), computed by ONE workgroup of two waves per request with the
 // limb-parallel arithmetic of lp25519.h, in one kernel launch:
 //
-//   wave 1  signature side: libsodium's checks on (R, S, smlen), k = SHA-512(R || A || M) mod L and its
-//           signed radix-16 digits (every lane computes the same scalar values); then [S]B from the
-//           engine's fixed-base comb T_B (16 table additions, the 16 entries fetched up front)
+//   wave 1  signature side: libsodium's checks on (R, S, smlen), k = SHA-512(R || A || M) mod L, then
+//           the half-size split k = k1 / k2 (mod 8L) (sc25519.h sc_halfsize: |k1|, k2 ~ 2^128, k2
+//           odd) and s2 = k2 S mod L (every lane computes the same scalar values)
 //   wave 0  key side, at the same time: decompression of A (row 0, negated) and of R (row 1) in one
-//           x^((p-5)/8) chain, the key checks, and the table [j](-A), j = -8..8, into LDS
-//   --- barrier 1 (k ready) ---
-//   wave 0  [k](-A): 63 x 4 doublings + 64 additions, or, when the key is in the node-side key cache
-//           (keycache.h), 32 additions from its comb table and no doublings
-//   wave 1  [S]B meanwhile
-//   --- barrier 2 ([S]B ready) ---
-//   wave 0  Q = [S]B + [k](-A) and the comparison with R without an inversion (lp_final_check), then
-//           the request's verdict bit (atomic OR).
+//           x^((p-5)/8) chain, the key checks, and the tables [j](-A) and [j]R', j = -8..8, into LDS
+//   --- barrier 1 (split ready, tables ready) ---
+//   wave 0  [k1](-A) (sign of k1 applied to the digits) + R': ~33 x 4 doublings + ~33 additions
+//   wave 1  [k2](-R') from wave 0's R table, then + [s2]B from the engine's fixed-base comb T_B (16
+//           table additions, the 16 entries fetched before the loop) -- the two halves of the old
+//           single 252-doubling chain run on two waves at once
+//   --- barrier 2 ---
+//   wave 0  Q = [k1](-A) + R' + [k2](-R') + [s2]B, compared with R' without an inversion
+//           (lp_final_check): equal iff [k2](SB - kA - R') = 0 iff libsodium's encode(SB - kA) == R
+//           (sc25519.h), then the request's verdict bit (atomic OR).
+//   A key in the node-side key cache (keycache.h) keeps the full scalar instead: wave 0 computes
+//   [k](-A) as 32 additions from its comb table, wave 1 [S]B, and Q = [S]B + [k](-A) is compared
+//   with R.
 //
 // The throughput paths keep one verification per lane and need ~1 ms however small the batch; here
 // the serial chain of one verification is spread over a wave (lp25519.h), so a batch of up to a few
@@ -29,6 +34,20 @@
 #include "verify_core.h"
 #include "pv_internal.h"
 #include "../../include/plenum_verify.h"
+
+// PV_LAT_HALF = 0: the single-chain form for A/B (wave 0 runs [k](-A) as 63 x 4 doublings + 64
+// additions, wave 1 [S]B); 1: the half-size split over both waves (above).
+#ifndef PV_LAT_HALF
+#define PV_LAT_HALF 1
+#endif
+// PV_LAT_TRACE (measurement builds only): block 0 stamps s_memrealtime (100 MHz) at its phase
+// boundaries into pv_lat_trace, read back by pv_debug_lat_trace.
+#ifdef PV_LAT_TRACE
+__device__ unsigned long long pv_lat_trace_buf[16];
+#define LAT_STAMP(i) do { if (blockIdx.x == 0 && (threadIdx.x & 63u) == 0) pv_lat_trace_buf[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define LAT_STAMP(i) do { } while (0)
+#endif
 
 namespace {
 
@@ -55,11 +74,13 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
     const uint32_t r = blockIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    __shared__ uint32_t s_k16[8];          // signed radix-16 digits of k (Straus, key not cached)
+    __shared__ uint32_t s_k16[8];          // signed radix-16 digits of |k1| (half-size split)
     __shared__ uint32_t s_k256[8];         // signed radix-256 digits of k (cached key's comb table)
     __shared__ uint32_t s_sig_ok;          // libsodium's checks on R, S, smlen
-    __shared__ uint32_t s_sb[64];          // [S]B, ext layout, one word per lane
+    __shared__ uint32_t s_nw, s_neg;       // windows of the split, k1 < 0
+    __shared__ uint32_t s_sb[64];          // wave 1's result, ext layout, one word per lane
     __shared__ uint32_t s_tab[17][64];     // [j](-A), j = -8..8, cached layout
+    __shared__ uint32_t s_rtab[17][64];    // [j]R', j = -8..8
 
     const uint64_t o0 = off[r], o1 = off[r + 1];
     const uint64_t smlen = o1 - o0;
@@ -79,45 +100,89 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
     }
     const LpLane c = LpLane::make();
     const LpConsts K = LpConsts::make(c);
+    // uniform: one branch per wave, the same on both waves
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(pv_kc_lookup(kc, in.A));
+    const bool cached = slot != PV_KC_EMPTY;
 
     if (wave == 1) {
-        // signature side: the 16 fixed-base entries are fetched first, then k, then [S]B
-        uint32_t fs[8];
-        sc_recode65536(fs, in.S);
+        LAT_STAMP(8);
+        const bool sig_ok = pv_sig_ok(in, smlen);
+        if (cached || !PV_LAT_HALF) {
+            // [S]B: the 16 fixed-base entries are fetched first, then k, then the additions
+            uint32_t fs[8];
+            sc_recode65536(fs, in.S);
+            lu ent[PV_BCOMB_POS];
+#pragma unroll
+            for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
+            uint32_t k[8];
+            pv_hash_k(k, in, smlen, mw);
+            LAT_STAMP(9);
+            uint32_t e256[8], e16[8];
+            sc_recode256(e256, k);
+            sc_recode16(e16, k);
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    s_k256[q] = e256[q];
+                    s_k16[q] = e16[q];
+                }
+                s_nw = 64;
+                s_neg = 0;
+                s_sig_ok = sig_ok ? 1u : 0u;
+            }
+            __syncthreads();  // 1: k is ready
+            auto entry = [&](int j) -> lu { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); };
+            s_sb[lane] = lp_comb_b(c, entry);
+            LAT_STAMP(11);
+            __syncthreads();  // 2: [S]B is ready
+            return;
+        }
+        uint32_t k[8];
+        pv_hash_k(k, in, smlen, mw);
+        LAT_STAMP(9);
+        pv_halfk hk;
+        sc_halfsize(hk, k);
+        uint32_t s2[8], fs[8], e1[8], e2[8];
+        sc_mul(s2, hk.k2, in.S);
+        sc_recode65536(fs, s2);
         lu ent[PV_BCOMB_POS];
 #pragma unroll
         for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
-        const bool sig_ok = pv_sig_ok(in, smlen);
-        uint32_t k[8];
-        pv_hash_k(k, in, smlen, mw);
-        uint32_t e16[8], e256[8];
-        sc_recode16(e16, k);
-        sc_recode256(e256, k);
+        sc_recode16(e1, hk.k1);
+        sc_recode16(e2, hk.k2);
+        const int nw1 = sc_nwin16(e1), nw2 = sc_nwin16(e2);
+        const int nw = __builtin_amdgcn_readfirstlane(nw1 > nw2 ? nw1 : nw2);
         if (lane == 0) {
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                s_k16[q] = e16[q];
-                s_k256[q] = e256[q];
-            }
+            for (int q = 0; q < 8; q++) s_k16[q] = e1[q];
+            s_nw = (uint32_t)nw;
+            s_neg = hk.neg ? 1u : 0u;
             s_sig_ok = sig_ok ? 1u : 0u;
         }
-        __syncthreads();  // 1: k is ready
-        auto entry = [&](int j) -> lu { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); };
-        s_sb[lane] = lp_comb_b(c, entry);
-        __syncthreads();  // 2: [S]B is ready
+        LAT_STAMP(10);
+        __syncthreads();  // 1: split ready; wave 0's tables ready
+        // [k2](-R') = sum of [-e]R' entries, then + [s2]B
+        lu acc = lp_straus_nw(c, nw, [&](int i) { return pv_nibble(e2[i >> 3], i); },
+                              [&](int e) -> lu { return s_rtab[8 - e][lane]; });
+#pragma unroll
+        for (int j = PV_BCOMB_POS - 1; j >= 0; j--) acc = lp_add_cached(c, acc, lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)));
+        s_sb[lane] = acc;
+        LAT_STAMP(11);
+        __syncthreads();  // 2
         return;
     }
+    LAT_STAMP(0);
     // key side: decompression of A (row 0) and R (row 1) in one chain
     lu sw[8];
     const lm odd_row = lp_eq(c.row & 1u, 1u);
 #pragma unroll
     for (int q = 0; q < 8; q++) sw[q] = lp_sel(odd_row, in.R[q], in.A[q]);
     const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    LAT_STAMP(1);
     const bool r_ok = pv_ge_is_canonical(in.R) && dec.ok_r && !(dec.x_r_zero && (in.R[7] >> 31));
-    const uint32_t slot = __builtin_amdgcn_readfirstlane(pv_kc_lookup(kc, in.A));  // uniform: one branch per wave
     bool key_ok;
     lu QA;
-    if (slot != PV_KC_EMPTY) {
+    if (cached) {
         // cached key: libsodium's key checks ran when its table was built; [k](-A) = 32 additions
         key_ok = kc.flags[slot] != 0;
         const uint32_t* tab = reinterpret_cast<const uint32_t*>(kc.tab + (uint64_t)slot * PV_COMB_POS * PV_COMB_ENT * 10);
@@ -133,19 +198,37 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
         key_ok = pv_ge_is_canonical(in.A) && !pv_has_small_order(in.A) && dec.ok_a;
         const lu negA = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
         lp_build_a_table(c, K, negA, [&](int j, const lu& q) { s_tab[j + 8][lane] = q; });
+        if (PV_LAT_HALF) {
+            const lu Rp = lp_ext_from_xy(c, K, dec.X, dec.Y, 1);
+            lp_build_a_table(c, K, Rp, [&](int j, const lu& q) { s_rtab[j + 8][lane] = q; });
+        }
+        LAT_STAMP(2);
         __syncthreads();  // 1
-        auto digit = [&](int i) { return pv_nibble(s_k16[i >> 3], i); };
+        LAT_STAMP(3);
+        const int nw = __builtin_amdgcn_readfirstlane((int)s_nw);
+        const int sgn = s_neg ? -1 : 1;
+        auto digit = [&](int i) { return sgn * pv_nibble(s_k16[i >> 3], i); };
         auto load = [&](int e) -> lu { return s_tab[e + 8][lane]; };
-        QA = lp_straus_a(c, digit, load);
+        QA = lp_straus_nw(c, nw, digit, load);
+        if (PV_LAT_HALF) QA = lp_add_cached(c, QA, s_rtab[9][lane]);  // + R'
     }
+    LAT_STAMP(4);
     __syncthreads();  // 2
+    LAT_STAMP(5);
     const bool eq = lp_final_check(c, K, QA, s_sb[lane], dec.X, dec.Y);
     const bool ok = eq && key_ok && r_ok && s_sig_ok != 0;
     if (lane == 0 && ok) atomicOr(&verdict[r >> 6], 1ull << (r & 63));
+    LAT_STAMP(6);
 #endif
 }
 
 }  // namespace
+
+#ifdef PV_LAT_TRACE
+extern "C" int pv_debug_lat_trace(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pv_lat_trace_buf), sizeof(pv_lat_trace_buf)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // Enqueue the latency path for n requests (device buffers as pv_verify_batch_device) on `stream`.
 int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,

@@ -170,6 +170,344 @@ PV_HD void sc_recode65536(uint32_t out[8], const uint32_t a[8]) {
     }
 }
 
+// ---------------------------------------------------------------- half-size scalars (Straus path)
+// The check encode([S]B - [k]A) == R is equivalent to D = [S]B - [k]A - R' = 0 once R decodes to R'
+// with encode(R') == R. For any (k1, k2) with k1 == k k2 (mod 8L) and k2 odd, 0 < k2 < L:
+//   [k2] D = [k2 S mod L] B - [k1] A - [k2] R'   (8L kills every point of the curve, B has order L)
+// and [k2] D = 0 iff D = 0 (the group is cyclic of order 8L: a nonzero D of order dividing k2 would
+// need L | k2 or a 2-power order dividing an odd k2). The short vector (k1, k2) of the lattice
+// {(x, y) : x == k y mod 8L} has |k1|, k2 ~ 2^128 (sqrt(8L) = 2^127.5), so the variable-base part
+// needs ~128 doublings instead of ~253 (T. Pornin, "Optimized lattice basis reduction in dimension 2,
+// and fast Schnorr and EdDSA signature verification", ePrint 2020/454, uses the same split modulo L
+// for cofactored checks; the modulus 8L and the odd k2 keep libsodium's cofactorless verdict exact
+// for mixed-order A and R).
+//
+// sc_halfsize: the extended Euclidean algorithm on (8L, k) -- remainders r_i = k t_i (mod 8L), t_0 = 0,
+// t_1 = 1 -- stopped at the first r_i < 2^128 whose t_i is odd. While r_i >= 2^131 the steps are taken
+// in Lehmer blocks (Knuth, TAOCP 4.5.2, Algorithm L): ~15 quotients at a time from the leading 52 bits
+// of the pair in double precision (each accepted only when both bracketing quotients agree), then ONE
+// multiword update of (r, t) by the block's 2x2 matrix; the last few bits go by exact single steps
+// (a double-precision quotient estimate corrected in exact multiword arithmetic). Every update applies
+// the same integer matrix to r and to t (t in two's complement), so r_i = k t_i (mod 8L) holds whatever
+// the quotients were; a step whose estimate cannot be settled (a quotient >= 2^32, |t| >= 2^168,
+// r_i = 0, too many steps, a block that breaks 0 <= r_{i+1} < r_i) sends the lane to the always-valid
+// split (k1, k2) = (k, 1), which costs the full-length loop but gives the same verdict.
+static constexpr uint32_t SC_8L[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u,
+                                      0x0u,        0x0u,        0x0u,        0x80000000u};
+#ifndef PV_HALF_MAXIT
+#define PV_HALF_MAXIT 64  // exact single steps (after the Lehmer blocks: ~3-12)
+#endif
+#ifndef PV_HALF_BLOCKS
+#define PV_HALF_BLOCKS 16  // Lehmer blocks (~5-6 needed from 2^255 to 2^131)
+#endif
+struct pv_halfk {
+    uint32_t k1[8];  // |k1|
+    uint32_t k2[8];  // k2: odd, > 0
+    bool neg;        // k1 = -|k1|
+    bool fallback;   // (k, 1) was used
+};
+
+PV_HD double sc_to_double(const uint32_t x[8]) {
+    double d = (double)x[7];
+#pragma unroll
+    for (int i = 6; i >= 0; i--) d = d * 4294967296.0 + (double)x[i];
+    return d;
+}
+
+// true on every lane of the wave (device) / the one lane (host)
+PV_HD bool pv_wave_all(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __all(p);
+#else
+    return p;
+#endif
+}
+
+// N-word two's complement helpers (arithmetic mod 2^(32 N))
+template <int N>
+PV_HD void mp_mulu32(uint32_t r[N], const uint32_t a[N], uint32_t m) {  // r = a m
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint64_t t = (uint64_t)a[i] * m + c;
+        r[i] = (uint32_t)t;
+        c = t >> 32;
+    }
+}
+template <int N>
+PV_HD void mp_muls32(uint32_t r[N], const uint32_t a[N], int64_t m) {  // r = a m, |m| < 2^32
+    const bool neg = m < 0;
+    mp_mulu32<N>(r, a, (uint32_t)(neg ? -m : m));
+    uint64_t c = neg ? 1u : 0u;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint64_t t = (uint64_t)(neg ? ~r[i] : r[i]) + c;
+        r[i] = (uint32_t)t;
+        c = t >> 32;
+    }
+}
+template <int N>
+PV_HD void mp_add(uint32_t r[N], const uint32_t a[N], const uint32_t b[N]) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint64_t t = (uint64_t)a[i] + b[i] + c;
+        r[i] = (uint32_t)t;
+        c = t >> 32;
+    }
+}
+template <int N>
+PV_HD void mp_sub(uint32_t r[N], const uint32_t a[N], const uint32_t b[N]) {
+    int64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const int64_t d = (int64_t)a[i] - (int64_t)b[i] + br;
+        r[i] = (uint32_t)d;
+        br = d >> 32;
+    }
+}
+template <int N>
+PV_HD bool mp_lt(const uint32_t a[N], const uint32_t b[N]) {  // unsigned a < b
+    int64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) br = ((int64_t)a[i] - (int64_t)b[i] + br) >> 32;
+    return br != 0;
+}
+// |t| < 2^168 for an 8-word two's complement t (bits 168..255 all equal the sign): one more step
+// (|q| < 2^32) or block (|A|, |B| < 2^31) cannot wrap mod 2^256
+PV_HD bool mp_small168(const uint32_t t[8]) {
+    const uint32_t s = (int32_t)t[7] >> 31;
+    return t[7] == s && t[6] == s && ((t[5] ^ s) >> 8) == 0;
+}
+
+// floor(a / b) for 0 <= a < 2^53, 0 < b < 2^53 (exact: double estimate, integer fix-up)
+PV_HD int64_t pv_fdiv53(int64_t a, int64_t b) {
+    int64_t q = (int64_t)((double)a / (double)b);
+    if (q * b > a) q--;
+    else if ((q + 1) * b <= a) q++;
+    return q;
+}
+
+PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8]) {
+    uint32_t r0[9], r1[9], t0[8], t1[8];  // r: 9 words (word 8 = 0 for a valid state)
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        r0[i] = i < 8 ? SC_8L[i] : 0u;
+        r1[i] = i < 8 ? k[i] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        t0[i] = 0;
+        t1[i] = i == 0 ? 1u : 0u;
+    }
+    bool bad = false;
+    // ---- Lehmer blocks while r1 >= 2^131
+    for (int blk = 0; blk < PV_HALF_BLOCKS; blk++) {
+        const bool act = !bad && ((r1[4] >> 3) | r1[5] | r1[6] | r1[7]) != 0;
+        if (pv_wave_all(!act)) break;
+        if (!act) continue;
+        // leading bits: xh = floor(r0 / 2^e), yh = floor(r1 / 2^e), xh < 2^52 (r0 >= 2^131: w >= 4)
+        int w = 4;
+#pragma unroll
+        for (int i = 5; i < 8; i++) w = r0[i] ? i : w;
+        uint32_t a1 = 0, a0 = 0, b1 = 0, b0 = 0;
+#pragma unroll
+        for (int i = 4; i < 8; i++) {
+            a1 = i == w ? r0[i] : a1;
+            a0 = i == w ? r0[i - 1] : a0;
+            b1 = i == w ? r1[i] : b1;
+            b0 = i == w ? r1[i - 1] : b0;
+        }
+        const int sh = 12 - (int)__builtin_clz(a1);  // bits above 52 in (a1:a0)
+        const int s = sh > 0 ? sh : 0;
+        const int64_t xh0 = (int64_t)((((uint64_t)a1 << 32) | a0) >> s);
+        const int64_t yh0 = (int64_t)((((uint64_t)b1 << 32) | b0) >> s);
+        // stop a block above 2^130: yh < 2^(130 - e), e = 32 (w - 1) + s (>= 79 here)
+        const int e = 32 * (w - 1) + s;
+        const int64_t ythr = e >= 130 ? 1 : ((int64_t)1 << (130 - e));
+        int64_t xh = xh0, yh = yh0, A = 1, B = 0, C = 0, D = 1;
+        bool go = true;
+        for (int it = 0; it < 40; it++) {
+            if (pv_wave_all(!go)) break;
+            if (!go) continue;
+            if (yh + C <= 0 || yh + D <= 0 || xh + A < 0 || xh + B < 0) {
+                go = false;
+                continue;
+            }
+            const int64_t q = pv_fdiv53(xh + A, yh + C);
+            if (q != pv_fdiv53(xh + B, yh + D)) { go = false; continue; }
+            const int64_t ny = xh - q * yh, nC = A - q * C, nD = B - q * D;
+            if (ny < ythr || nC >= 0x7FFFFFFF || nC <= -0x7FFFFFFF || nD >= 0x7FFFFFFF || nD <= -0x7FFFFFFF) {
+                go = false;
+                continue;
+            }
+            A = C;
+            C = nC;
+            B = D;
+            D = nD;
+            xh = yh;
+            yh = ny;
+        }
+        if (B == 0) {
+            // no quotient could be settled from the leading bits: one exact step below
+            // (the block loop then continues from the new pair)
+            const double qd = sc_to_double(r0) / sc_to_double(r1);
+            bad |= !(qd < 4294967295.0);
+            uint32_t q = bad ? 0u : (uint32_t)qd;
+            uint32_t p[9], rn[9];
+            mp_mulu32<9>(p, r1, q);
+            mp_sub<9>(rn, r0, p);
+            if ((int32_t)rn[8] < 0) {
+                mp_add<9>(rn, rn, r1);
+                q--;
+            }
+            if (!mp_lt<9>(rn, r1)) {
+                mp_sub<9>(rn, rn, r1);
+                q++;
+            }
+            bad |= (int32_t)rn[8] < 0 || !mp_lt<9>(rn, r1);
+            uint32_t qt[8], tn[8];
+            mp_mulu32<8>(qt, t1, q);
+            mp_sub<8>(tn, t0, qt);
+#pragma unroll
+            for (int i = 0; i < 9; i++) {
+                r0[i] = r1[i];
+                r1[i] = rn[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                t0[i] = t1[i];
+                t1[i] = tn[i];
+            }
+        } else {
+            uint32_t u[9], v[9], nr0[9], nr1[9], nt0[8], nt1[8], x[8], y[8];
+            mp_muls32<9>(u, r0, A);
+            mp_muls32<9>(v, r1, B);
+            mp_add<9>(nr0, u, v);
+            mp_muls32<9>(u, r0, C);
+            mp_muls32<9>(v, r1, D);
+            mp_add<9>(nr1, u, v);
+            mp_muls32<8>(x, t0, A);
+            mp_muls32<8>(y, t1, B);
+            mp_add<8>(nt0, x, y);
+            mp_muls32<8>(x, t0, C);
+            mp_muls32<8>(y, t1, D);
+            mp_add<8>(nt1, x, y);
+            bad |= (int32_t)nr0[8] < 0 || (int32_t)nr1[8] < 0 || !mp_lt<9>(nr1, nr0);
+#pragma unroll
+            for (int i = 0; i < 9; i++) {
+                r0[i] = nr0[i];
+                r1[i] = nr1[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                t0[i] = nt0[i];
+                t1[i] = nt1[i];
+            }
+        }
+        bad |= !mp_small168(t1) || !mp_small168(t0);
+    }
+    // ---- exact single steps until r1 < 2^128 with t1 odd
+    bool done = ((r1[4] | r1[5] | r1[6] | r1[7]) == 0) && (t1[0] & 1u);
+    for (int it = 0; it < PV_HALF_MAXIT; it++) {
+        if (pv_wave_all(done || bad)) break;
+        if (done || bad) continue;
+        const double qd = sc_to_double(r0) / sc_to_double(r1);  // r1 = 0: +inf -> bad
+        bad |= !(qd < 4294967295.0);
+        uint32_t q = bad ? 0u : (uint32_t)qd;
+        uint32_t p[9], rn[9];
+        mp_mulu32<9>(p, r1, q);
+        mp_sub<9>(rn, r0, p);
+        // estimate one too high: rn < 0 -> rn += r1, q -= 1; one too low: rn >= r1 -> rn -= r1, q += 1
+        {
+            const bool lo = (int32_t)rn[8] < 0;
+            uint32_t ra[9];
+            mp_add<9>(ra, rn, r1);
+#pragma unroll
+            for (int i = 0; i < 9; i++) rn[i] = lo ? ra[i] : rn[i];
+            bad |= lo && q == 0u;
+            q -= lo ? 1u : 0u;
+        }
+        {
+            uint32_t rs[9];
+            mp_sub<9>(rs, rn, r1);
+            const bool ge = (int32_t)rs[8] >= 0;
+#pragma unroll
+            for (int i = 0; i < 9; i++) rn[i] = ge ? rs[i] : rn[i];
+            bad |= ge && q == 0xFFFFFFFFu;
+            q += ge ? 1u : 0u;
+        }
+        bad |= (int32_t)rn[8] < 0 || !mp_lt<9>(rn, r1);
+        uint32_t qt[8], tn[8];
+        mp_mulu32<8>(qt, t1, q);
+        mp_sub<8>(tn, t0, qt);
+        bad |= !mp_small168(tn);
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            r0[i] = r1[i];
+            r1[i] = rn[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            t0[i] = t1[i];
+            t1[i] = tn[i];
+        }
+        done = ((r1[4] | r1[5] | r1[6] | r1[7]) == 0) && (t1[0] & 1u);
+    }
+    // k2 = |t1|, k1 = r1 with t1's sign moved onto it
+    const bool tneg = (int32_t)t1[7] < 0;
+    uint32_t ta[8];
+    {
+        uint64_t c = tneg ? 1u : 0u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint64_t t = (uint64_t)(tneg ? ~t1[i] : t1[i]) + c;
+            ta[i] = (uint32_t)t;
+            c = t >> 32;
+        }
+    }
+    const bool ok = done && !bad && (ta[5] | ta[6] | ta[7]) == 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        h.k1[i] = ok ? r1[i] : k[i];
+        h.k2[i] = ok ? ta[i] : (i == 0 ? 1u : 0u);
+    }
+    h.neg = ok && tneg;
+    h.fallback = !ok;
+}
+
+// r = a * b mod L (a, b < 2^256)
+PV_HD void sc_mul(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t t = (uint64_t)a[i] * b[j] + x[i + j] + c;
+            x[i + j] = (uint32_t)t;
+            c = t >> 32;
+        }
+        x[i + 8] = (uint32_t)c;
+    }
+    sc_reduce64(r, x);
+}
+
+// Windows the radix-16 loop needs for packed digits e (sc_recode16): 1 + the highest nonzero digit.
+PV_HD int sc_nwin16(const uint32_t e[8]) {
+    int nw = 1;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        if (e[w]) {
+            const int top = 31 - (int)__builtin_clz(e[w]);  // highest set bit
+            nw = 8 * w + top / 4 + 1;
+        }
+    }
+    return nw;
+}
+
 // Bits [lo, lo + n) of the 256-bit little-endian a (n <= 32).
 PV_HD uint32_t sc_bits(const uint32_t a[8], int lo, int n) {
     const int i = lo >> 5, sh = lo & 31;

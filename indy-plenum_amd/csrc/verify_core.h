@@ -238,6 +238,49 @@ PV_HD void pv_straus_a_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const Dig& dig
     ge_p1p1_to_p2(X, Y, Z, t);
 }
 
+// Half-size-scalar Straus loop (sc25519.h sc_halfsize): Q' = [k1](+-A) + [k2](-R') over nw signed
+// radix-16 windows of both scalars (two per-lane tables, two cached additions per window, ~33 windows
+// instead of 64), then + accB = [k2 S mod L]B and + R' (the R table's entry -1). The result encodes
+// to R exactly when Q' + [k2 S]B = [k2](SB - kA - R') is the identity, i.e. when libsodium's
+// encode(SB - kA) == R holds (see sc_halfsize). dig.ek(q) / dig.ek2(q): packed digits of |k1| / k2;
+// nw: windows (uniform across the wave on the device: the wave's maximum).
+template <class ATab, class RTab, class Dig, class AccB>
+PV_HD void pv_straus_ar_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const RTab& rtab, const Dig& dig, int nw,
+                            const AccB& load_accB) {
+    ge_p3 acc;
+    ge_p3_identity(acc);
+    ge_p1p1 t;
+    uint32_t w1 = 0, w2 = 0;
+    for (int win = nw - 1; win >= 0; win--) {
+        if (win == nw - 1 || (win & 7) == 7) {
+            w1 = dig.ek(win >> 3);
+            w2 = dig.ek2(win >> 3);
+        }
+        const int e1 = pv_nibble(w1, win), e2 = pv_nibble(w2, win);
+        if (win != nw - 1) {
+            for (int j = 0; j < 3; j++) {
+                ge_p2_dbl(t, X, Y, Z);
+                ge_p1p1_to_p2(X, Y, Z, t);
+            }
+            ge_p2_dbl(t, X, Y, Z);
+            ge_p1p1_to_p3(acc, t);
+        }
+        pv_add_a(t, acc, atab, e1);
+        ge_p1p1_to_p3(acc, t);
+        pv_add_a(t, acc, rtab, e2);
+        if (win > 0) ge_p1p1_to_p2(X, Y, Z, t);
+    }
+    ge_p1p1_to_p3(acc, t);
+    ge_p3 accB;
+    load_accB(accB);
+    ge_cached cb;
+    ge_p3_to_cached(cb, accB);
+    ge_add_cached(t, acc, cb);
+    ge_p1p1_to_p3(acc, t);
+    pv_add_a(t, acc, rtab, -1);
+    ge_p1p1_to_p2(X, Y, Z, t);
+}
+
 template <class ATab, class BTab, class Dig>
 PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const Dig& dig) {
     fe X, Y, Z;
@@ -395,6 +438,40 @@ PV_HD bool pv_prepare(ge_p3& negA, uint32_t k[8], const pv_sig_words& in, uint64
     bool ok = pv_sig_ok(in, smlen);
     ok &= pv_key_ok_negate(negA, in.A);
     pv_hash_k(k, in, smlen, msgword);
+    return ok;
+}
+
+// R as a point for the half-size check: libsodium accepts only when encode(Q) == R bytewise, and an
+// R' with encode(R') == R exists iff R is canonical (y < p), decodes, and is not x = 0 with the sign
+// bit set. Returns -R' and whether such an R' exists (if not, the verdict is a reject).
+PV_HD bool pv_r_decode_negate(ge_p3& negR, const uint32_t R[8]) {
+    bool ok = pv_ge_is_canonical(R);
+    ok &= ge_frombytes_negate(negR, R);
+    ok &= !(fe_iszero(negR.X) && (R[7] >> 31));
+    return ok;
+}
+
+// p = neg ? -p : p, X and T carried back to reduced limbs (p reduced on entry)
+PV_HD void ge_p3_cneg(ge_p3& p, bool neg) {
+    fe_cneg(p.X, p.X, neg);
+    fe_carry(p.X, p.X);
+    fe_cneg(p.T, p.T, neg);
+    fe_carry(p.T, p.T);
+}
+
+// Stage 1 of a half-size verification: every check, PA = [sign k1](-A) (-A, or A when k1 < 0),
+// -R', the split of k (sc_halfsize) and s2 = k2 S mod L. false if any check rejects.
+template <class MsgWord>
+PV_HD bool pv_prepare_half(ge_p3& PA, ge_p3& negR, pv_halfk& hk, uint32_t s2[8], const pv_sig_words& in,
+                           uint64_t smlen, const MsgWord& msgword) {
+    bool ok = pv_sig_ok(in, smlen);
+    ok &= pv_key_ok_negate(PA, in.A);
+    ok &= pv_r_decode_negate(negR, in.R);
+    uint32_t k[8];
+    pv_hash_k(k, in, smlen, msgword);
+    sc_halfsize(hk, k);
+    sc_mul(s2, hk.k2, in.S);
+    ge_p3_cneg(PA, hk.neg);
     return ok;
 }
 

@@ -7,6 +7,7 @@
 #include "comb.h"
 #include "lp25519.h"
 #include <string.h>
+#include <algorithm>
 #include <vector>
 #include <thread>
 
@@ -283,6 +284,91 @@ int hc_sign_open_straus_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t*
     return ok && pv_words_equal(enc, in.R);
 }
 
+// sc_halfsize on a 32-byte scalar: |k1| and k2 (32 bytes each), *neg = k1 < 0; returns 1 if the
+// (k, 1) fallback was taken.
+int hc_sc_halfsize(const uint8_t* k, uint8_t* k1, uint8_t* k2, int* neg) {
+    uint32_t kw[8];
+    load_words(kw, k);
+    pv_halfk h;
+    sc_halfsize(h, kw);
+    memcpy(k1, h.k1, 32);
+    memcpy(k2, h.k2, 32);
+    *neg = h.neg;
+    return h.fallback;
+}
+void hc_sc_mul(uint8_t* r, const uint8_t* a, const uint8_t* b) {
+    uint32_t aw[8], bw[8], rw[8];
+    load_words(aw, a);
+    load_words(bw, b);
+    sc_mul(rw, aw, bw);
+    memcpy(r, rw, 32);
+}
+int hc_sc_nwin16(const uint8_t* a) {
+    uint32_t w[8], e[8];
+    load_words(w, a);
+    sc_recode16(e, w);
+    return sc_nwin16(e);
+}
+
+// The half-size Straus path as the device runs it: pv_prepare_half (checks, +-A, -R', split of k,
+// k2 S mod L), the [j]PA and [j](-R') tables, [k2 S]B from pv_comb_b_acc_w<16> over the radix-65536
+// host table, pv_straus_ar_xyz, encoding compared with R. force_fallback: use (k, 1) as the split (the
+// lane fallback). extra_windows: run that many leading all-zero windows (a wave whose maximum exceeds
+// this lane's need).
+struct HostDig2 {
+    uint32_t e[8], e2[8];
+    uint32_t ek(int q) const { return e[q]; }
+    uint32_t ek2(int q) const { return e2[q]; }
+};
+int hc_sign_open_straus_half16(const uint8_t* sm, uint64_t smlen, const uint8_t* pk, int force_fallback,
+                               int extra_windows) {
+    const std::vector<uint32_t>& bcomb = host_bcomb();
+    std::vector<uint8_t> buf(smlen + 256, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    HostMsg mw{buf.data()};
+    ge_p3 PA, negR;
+    pv_halfk hk;
+    uint32_t s2[8];
+    bool ok = pv_prepare_half(PA, negR, hk, s2, in, smlen, mw);
+    if (force_fallback) {
+        // redo the split as the fallback lane would have it
+        ge_p3_cneg(PA, hk.neg);  // back to -A
+        uint32_t k[8];
+        pv_hash_k(k, in, smlen, mw);
+        for (int i = 0; i < 8; i++) {
+            hk.k1[i] = k[i];
+            hk.k2[i] = i == 0 ? 1u : 0u;
+        }
+        hk.neg = false;
+        sc_mul(s2, hk.k2, in.S);
+    }
+    HostATab at, rt;
+    pv_build_a_table(at, PA);
+    pv_build_a_table(rt, negR);
+    HostDig2 dig;
+    sc_recode16(dig.e, hk.k1);
+    sc_recode16(dig.e2, hk.k2);
+    int nw = sc_nwin16(dig.e);
+    const int nw2 = sc_nwin16(dig.e2);
+    nw = nw > nw2 ? nw : nw2;
+    nw += extra_windows;
+    if (nw > 64) nw = 64;
+    int32_t fb[16];
+    sc_recode_w<16, 16>(fb, s2);
+    HostBRows brows{bcomb.data()};
+    ge_p3 accB;
+    pv_comb_b_acc_w<16>(accB, PvRowsStageB<HostBRows>{brows, 0, 0}, [&](int j) { return fb[j]; });
+    fe X, Y, Z;
+    pv_straus_ar_xyz(X, Y, Z, at, rt, dig, nw, [&](ge_p3& p) { p = accB; });
+    uint32_t enc[8];
+    ge_p2_tobytes(enc, X, Y, Z);
+    return ok && pv_words_equal(enc, in.R);
+}
+
 // pv_comb_fill_sparse (the small-chunk table fill) against pv_comb_fill_block (the full fill) for one
 // key: every position, a pseudo-random need set of about `density` x 129 entries (seeded); returns the
 // number of needed or always-built entries whose point differs from the full table's.
@@ -377,7 +463,8 @@ void hc_lp_sub(uint32_t* out, const uint32_t* p, const uint32_t* q) {
     hc_rows_out(out, lp_add_cached(c, hc_rows_in(p), lp_neg_cached(c, lp_to_cached(c, hc_rows_in(q), K.d2))));
 }
 
-// crypto_sign_open through the latency path: the kernel's two waves, one after the other
+// crypto_sign_open through the latency path: the kernel's two waves, one after the other (wave 1
+// up to its barrier, wave 0 up to its barrier, wave 1's loop, wave 0's loop and the final check)
 int hc_lp_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     const std::vector<uint32_t>& bcomb = host_bcomb();
     std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK
@@ -389,28 +476,39 @@ int hc_lp_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     HostMsg mw{buf.data()};
     const LpLane c = LpLane::make();
     const LpConsts K = LpConsts::make(c);
-    // wave 1: signature side
-    uint32_t fs[8];
-    sc_recode65536(fs, in.S);
+    // wave 1: checks, k, the half-size split, s2 = k2 S mod L and its comb entries
+    const bool sig_ok = pv_sig_ok(in, smlen);
+    uint32_t k[8];
+    pv_hash_k(k, in, smlen, mw);
+    pv_halfk hk;
+    sc_halfsize(hk, k);
+    uint32_t s2[8], fs[8], e1[8], e2[8];
+    sc_mul(s2, hk.k2, in.S);
+    sc_recode65536(fs, s2);
     lu ent[PV_BCOMB_POS];
     for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb.data(), j, pv_half(fs[j >> 1], j));
-    const bool sig_ok = pv_sig_ok(in, smlen);
-    uint32_t k[8], ek[8];
-    pv_hash_k(k, in, smlen, mw);
-    sc_recode16(ek, k);
-    const lu SB = lp_comb_b(c, [&](int j) { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); });
-    // wave 0: key side
+    sc_recode16(e1, hk.k1);
+    sc_recode16(e2, hk.k2);
+    const int nw = std::max(sc_nwin16(e1), sc_nwin16(e2));
+    // wave 0: decompression of A and R, key checks, both tables
     lu sw[8];
     const lm odd_row = lp_eq(c.row & 1u, 1u);
     for (int q = 0; q < 8; q++) sw[q] = lp_sel(odd_row, in.R[q], in.A[q]);
     const LpDecomp dec = lp_decompress_ar(c, K, sw);
     const bool key_ok = pv_ge_is_canonical(in.A) && !pv_has_small_order(in.A) && dec.ok_a;
     const bool r_ok = pv_ge_is_canonical(in.R) && dec.ok_r && !(dec.x_r_zero && (in.R[7] >> 31));
-    const lu negA = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
-    std::vector<lu> tab(17);
-    lp_build_a_table(c, K, negA, [&](int j, const lu& q) { tab[j + 8] = q; });
-    const lu QA = lp_straus_a(c, [&](int i) { return pv_nibble(ek[i >> 3], i); },
-                              [&](int e) { return tab[e + 8]; });
+    std::vector<lu> tab(17), rtab(17);
+    lp_build_a_table(c, K, lp_ext_from_xy(c, K, dec.X, dec.Y, 0), [&](int j, const lu& q) { tab[j + 8] = q; });
+    lp_build_a_table(c, K, lp_ext_from_xy(c, K, dec.X, dec.Y, 1), [&](int j, const lu& q) { rtab[j + 8] = q; });
+    // wave 1 after barrier 1: [k2](-R') + [s2]B
+    lu SB = lp_straus_nw(c, nw, [&](int i) { return pv_nibble(e2[i >> 3], i); },
+                         [&](int e) { return rtab[8 - e]; });
+    for (int j = PV_BCOMB_POS - 1; j >= 0; j--) SB = lp_add_cached(c, SB, lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)));
+    // wave 0 after barrier 1: [k1](-A) (signed) + R'
+    const int sgn = hk.neg ? -1 : 1;
+    const lu QA = lp_add_cached(c, lp_straus_nw(c, nw, [&](int i) { return sgn * pv_nibble(e1[i >> 3], i); },
+                                                [&](int e) { return tab[e + 8]; }),
+                                rtab[9]);
     const bool eq = lp_final_check(c, K, QA, SB, dec.X, dec.Y);
     return eq && key_ok && r_ok && sig_ok;
 }

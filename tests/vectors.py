@@ -34,7 +34,7 @@ def seed_for(tag, i):
 class VectorGen:
     CLASSES = ("valid", "flip_R", "flip_S", "flip_A", "flip_M", "S_plus_L", "S_big", "R_blacklist",
                "A_blacklist", "A_noncanonical", "A_offcurve", "R_noncanonical", "mixed_order_A", "short_sm",
-               "empty_msg", "long_msg")
+               "empty_msg", "long_msg", "mixed_order_AR", "mixed_order_R")
 
     def __init__(self, sodium, oracle, seed=1):
         self.ls = sodium
@@ -130,6 +130,25 @@ class VectorGen:
             m = self.msg()
             sig = bytearray(self.o.sign_raw(rr, a.to_bytes(32, "little"), A2, m))
             pk = A2
+        elif cls in ("mixed_order_AR", "mixed_order_R"):
+            # R' = rB + [j]T8 (j = 1..7) with S = r + k a: libsodium compares encode(SB - kA) with R,
+            # so for A = aB + T8 the signature passes iff [j]T8 = -[k]T8 (about 1 in 8 -- half of
+            # these cases retry until it passes), and for a prime-order A (mixed_order_R) never.
+            a = r.randrange(1, L)
+            A = self.o.scalarmult_base(a.to_bytes(32, "little"))
+            pk = self.o.point_add(A, ORDER8) if cls == "mixed_order_AR" else A
+            m = self.msg()
+            want_pass = cls == "mixed_order_AR" and r.random() < 0.5
+            for _ in range(200):
+                rr = r.randrange(1, L)
+                T = ORDER8
+                for _ in range(r.randrange(7)):
+                    T = self.o.point_add(T, ORDER8)
+                R = self.o.point_add(self.o.scalarmult_base(rr.to_bytes(32, "little")), T)
+                k = int.from_bytes(hashlib.sha512(R + pk + m).digest(), "little") % L
+                sig = bytearray(R + ((rr + k * a) % L).to_bytes(32, "little"))
+                if not want_pass or self.ls.sign_open_ok(bytes(sig) + m, pk):
+                    break
         elif cls == "short_sm":
             smb = bytes(sig) + m
             return smb[: r.randrange(0, 64)], pk
