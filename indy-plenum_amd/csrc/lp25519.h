@@ -554,6 +554,20 @@ LP_FN lu lp_straus_nw(const LpLane& c, int nw, const Digit& digit, const Load& l
     return acc;
 }
 
+// The windows [lo, hi) of a signed radix-16 scalar against the table of P (window i weighs 16^(i-lo):
+// the caller's table is of [16^lo] P): (hi - lo - 1) x 4 doublings + (hi - lo) additions; the identity
+// when hi <= lo (uniform bounds).
+template <class Digit, class Load>
+LP_FN lu lp_straus_range(const LpLane& c, int lo, int hi, const Digit& digit, const Load& load) {
+    if (hi <= lo) return lp_identity_ext(c);
+    lu acc = lp_add_cached(c, lp_identity_ext(c), load(digit(hi - 1)));
+    for (int win = hi - 2; win >= lo; win--) {
+        acc = lp_dbl(c, lp_dbl(c, lp_dbl(c, lp_dbl(c, acc))));
+        acc = lp_add_cached(c, acc, load(digit(win)));
+    }
+    return acc;
+}
+
 // Entry d = |f| of position j of the fixed-base comb T_B (comb.h: affine niels, words y+x at 0..9,
 // y-x at 10..19, 2dxy at 20..29 of a PV_BCOMB_STRIDE-word entry) in lp cached layout
 // [y-x, y+x, 2dxy, 2], negated for f < 0 (y+x <-> y-x, -2dxy).

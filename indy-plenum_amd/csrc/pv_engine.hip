@@ -156,6 +156,10 @@ struct Soa {
 #define PV_STRAUS_HALF 1
 #endif
 static constexpr uint32_t PV_ATAB_ENT = PV_STRAUS_HALF ? 18u : 9u;  // table entries per slot
+// half-size msm: table entries fetched one addition ahead into LDS (pv_straus_ar_xyz_staged)
+#ifndef PV_MSM_STAGED
+#define PV_MSM_STAGED 0
+#endif
 struct DevATab {
     uint4* base;
     uint32_t nslots;
@@ -393,6 +397,53 @@ static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 #define PV_COMB_MIN_REQ 48
 #endif
 
+// LDS-DMA staging of one table entry per lane (comb.h, PV_COMB_PIPELINE). An entry of Q uint4 is
+// fetched by Q global_load_lds_dwordx4, each writing 1 KiB = 16 B x 64 lanes of the wave's staging
+// area, laid out [q][lane] so that reading it back is one conflict-free ds_read_b128 per q.
+__device__ __forceinline__ void pv_glds16(const uint4* g, uint4* l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+// Q pieces of 16 B from g[0..Q) to l[q * 64 + lane] (a wave's [q][lane] staging area). The
+// instruction's immediate offset (16 q) applies to BOTH the global and the LDS address, so the LDS
+// base of piece q is moved back by the same 16 q bytes (M0 is set per instruction anyway): all Q
+// loads then share ONE 64-bit global address instead of Q 64-bit adds per staged entry.
+template <int Q, int q = 0>
+__device__ __forceinline__ void pv_glds16_row(const uint4* g, uint4* l) {
+    if constexpr (q < Q) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)(l + q * 64 - q), 16, 16 * q, 0);
+        pv_glds16_row<Q, q + 1>(g, l);
+    }
+}
+// the LDS reads of the previous staged entry must be complete before its buffer is refilled
+__device__ __forceinline__ void pv_lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+#if PV_STRAUS_HALF
+// The half-size msm's per-lane tables (DevATab layout, tile-major): entry j of table t of slot i staged
+// into the wave's [10][64] area (pv_straus_ar_xyz_staged)
+struct DevATabStage {
+    uint4* base;
+    uint32_t slot;
+    uint4* lds;
+    uint32_t lane;
+    __device__ __forceinline__ void stage(int t, int j) const {
+        const uint4* e = &DevATab{base, 0u, slot, t ? 9u : 0u}.at(j, 0);
+        pv_lds_reads_done();
+        pv_glds16_row<10>(e, lds);
+    }
+    __device__ __forceinline__ void staged(int h, uint32_t w[20]) const {
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const uint4 v = lds[(5 * h + q) * 64 + lane];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+    }
+};
+#endif
 // Straus path: [S]B from the wide fixed-base comb (pv_straus_b_kernel) and a Straus loop over k only
 // (pv_straus_a_xyz), instead of 32 B additions interleaved in the loop (LDS table of [j]B).
 #ifndef PV_STRAUS_WIDE_B
@@ -428,41 +479,22 @@ __device__ __forceinline__ void pv_prep_slot(const uint8_t* __restrict__ sm, con
     in.A[4] = a1.x; in.A[5] = a1.y; in.A[6] = a1.z; in.A[7] = a1.w;
 #if PV_STRAUS_HALF
     {
-        // pv_prepare_half split over two kernels: here the signature checks, k, its split, digits of
-        // |k1| (rows 0..7) and k2 (PV_K2_ROW..), the window count (row PV_NW_ROW), digits of k2 S mod L,
-        // then A's checks and +-A; R's checks and -R' run in pv_table_kernel
+        // pv_prepare_half over three kernels: here the signature checks, k (to rows 0..7 for
+        // pv_split_kernel), A's checks and -A (table entry 1); the split of k and the digits in
+        // pv_split_kernel; the sign of k1 on -A, R's checks, -R' and both tables in pv_table_kernel
         bool ok = pv_sig_ok(in, smlen);
-        bool neg;
+        const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
         {
             uint32_t k[8];
             pv_hash_k(k, in, smlen, mw);
-            pv_halfk hk;
-            sc_halfsize(hk, k);
-            neg = hk.neg;
-            uint32_t s2[8];
-            sc_mul(s2, hk.k2, in.S);
-            const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
-            int32_t fb[Bc2<W>::POS];
-            sc_recode_w<W, Bc2<W>::POS>(fb, s2);
 #pragma unroll
-            for (int j = 0; j < Bc2<W>::POS; j++) ds.st(8 + j, (uint32_t)i, (uint32_t)fb[j]);
-            uint32_t e1[8], e2[8];
-            sc_recode16(e1, hk.k1);
-            sc_recode16(e2, hk.k2);
-            const int nw1 = sc_nwin16(e1), nw2 = sc_nwin16(e2);
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                ds.st(q, (uint32_t)i, e1[q]);
-                ds.st(PV_K2_ROW + q, (uint32_t)i, e2[q]);
-            }
-            ds.st(PV_NW_ROW, (uint32_t)i, (uint32_t)(nw1 > nw2 ? nw1 : nw2));
+            for (int q = 0; q < 8; q++) ds.st(q, (uint32_t)i, k[q]);
         }
         {
-            ge_p3 PA;  // +-A (k1's sign) to table entry 1 for pv_table_kernel
-            ok &= pv_key_ok_negate(PA, in.A);
-            ge_p3_cneg(PA, neg);
+            ge_p3 negA;
+            ok &= pv_key_ok_negate(negA, in.A);
             const DevATab at{wk.atab, (uint32_t)wk.stride, (uint32_t)i};
-            at.store_p3(1, PA);
+            at.store_p3(1, negA);
         }
         wk.flags[i] = ok ? 1u : 0u;
         return;
@@ -531,6 +563,55 @@ __global__ __launch_bounds__(PV_BLOCK, PV_PREP_MINBLOCKS) void pv_prep_kernel(co
     }
 }
 
+#if PV_STRAUS_HALF
+// Kernel 1a (half-size path): the split k = k1 / k2 (mod 8L) of each Straus slot's k (rows 0..7, from
+// pv_prep_kernel), s2 = k2 S mod L; writes the digits of |k1| (rows 0..7), k2 (PV_K2_ROW..), the window
+// count and k1's sign (row PV_NW_ROW: nw | neg << 8) and the wide-comb digits of s2 (rows 8..). Its own
+// kernel: few registers, so the latency of the Euclid steps is hidden by occupancy.
+template <int W>
+__global__ __launch_bounds__(PV_BLOCK) void pv_split_kernel(const uint8_t* __restrict__ sm,
+                                                            const uint64_t* __restrict__ off, uint64_t n, Work wk,
+                                                            Gate gate) {
+    if (gate.off()) return;
+    pv_straus_prio();
+    const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t sb = gate.stile(t, ntiles);
+        if ((sb + 1) * PV_BLOCK <= nc) break;
+        const uint32_t i = sb * PV_BLOCK + threadIdx.x;  // slot
+        if (i >= n || i < nc) continue;
+        const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
+        uint32_t k[8], S[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) k[q] = ds.ld(q, i);
+        {
+            const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[gate.req(i)]);
+            const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+#pragma unroll
+            for (int q = 0; q < 8; q++) S[q] = mw.dw(8 + q);
+        }
+        pv_halfk hk;
+        sc_halfsize(hk, k);
+        uint32_t s2[8];
+        sc_mul(s2, hk.k2, S);
+        int32_t fb[Bc2<W>::POS];
+        sc_recode_w<W, Bc2<W>::POS>(fb, s2);
+#pragma unroll
+        for (int j = 0; j < Bc2<W>::POS; j++) ds.st(8 + j, i, (uint32_t)fb[j]);
+        uint32_t e1[8], e2[8];
+        sc_recode16(e1, hk.k1);
+        sc_recode16(e2, hk.k2);
+        const int nw1 = sc_nwin16(e1), nw2 = sc_nwin16(e2);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            ds.st(q, i, e1[q]);
+            ds.st(PV_K2_ROW + q, i, e2[q]);
+        }
+        ds.st(PV_NW_ROW, i, (uint32_t)(nw1 > nw2 ? nw1 : nw2) | (hk.neg ? 0x100u : 0u));
+    }
+}
+#endif
+
 // Kernel 1b: the cached table [j](-A), j = 0..8 (full-length path: -A from entry 1); half-size path:
 // decompression and checks of A and R, tables [j](+-A) (entries 0..8) and [j](-R') (entries 9..17).
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(const uint8_t* __restrict__ sm,
@@ -545,7 +626,8 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(const uint8_t* __
         const uint32_t i = sb * PV_BLOCK + threadIdx.x;  // slot
         if (i >= n || i < nc) continue;
 #if PV_STRAUS_HALF
-        // [j](+-A) from entry 1 (pv_prep_kernel), then R's canonical-decoding rule and [j](-R')
+        // [j](+-A) from -A (entry 1, pv_prep_kernel) and k1's sign (pv_split_kernel), then R's
+        // canonical-decoding rule and [j](-R')
         const uint32_t r = gate.req(i);
         const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[r]);
         const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
@@ -553,6 +635,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(const uint8_t* __
             DevATab at{wk.atab, (uint32_t)wk.stride, i};
             ge_p3 PA;
             at.load_p3(1, PA);
+            ge_p3_cneg(PA, (Soa(wk.digits, PV_DIGIT_ROWS, wk.stride).ld(PV_NW_ROW, i) & 0x100u) != 0);  // +-A
             pv_build_a_table(at, PA);
         }
         bool ok;
@@ -593,6 +676,10 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
     // nothing for this block (or no Straus slot at all): leave before the LDS fill
     if (blockIdx.x >= ntiles || nc >= n || (gate.stile(blockIdx.x, ntiles) + 1) * PV_BLOCK <= nc) return;
     pv_straus_prio();
+#if PV_STRAUS_HALF && PV_MSM_STAGED
+    __shared__ uint4 stg[PV_BLOCK / 64][10][64];
+    uint4* stg_wave = &stg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0][0];
+#endif
 #if !PV_STRAUS_WIDE_B
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
     for (int t = threadIdx.x; t < PV_BTAB_ENTRIES * PV_BTAB_STRIDE / 4; t += PV_BLOCK)
@@ -606,16 +693,30 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
         const uint32_t i0 = sb * PV_BLOCK + threadIdx.x;  // slot
         const bool active = i0 < n && i0 >= nc;
         const uint32_t i = active ? i0 : (uint32_t)n - 1;  // n - 1 >= nc here: a Straus slot
+#if !(PV_STRAUS_HALF && PV_MSM_STAGED)
         const DevATab at{wk.atab, (uint32_t)wk.stride, i};
+#endif
         const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
         const Soa qs(wk.q, 40, wk.stride);
         fe X, Y, Z;
 #if PV_STRAUS_HALF
         // the wave's window count: its lanes' maximum (a lane's digits above its own count are 0)
-        int nw = (int)dig.nw();
+        int nw = (int)(dig.nw() & 0xFFu);
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) nw = max(nw, __shfl_xor(nw, m));
         nw = __builtin_amdgcn_readfirstlane(nw);
+#if PV_MSM_STAGED
+        pv_straus_ar_xyz_staged(X, Y, Z, DevATabStage{wk.atab, i, stg_wave, threadIdx.x & 63u}, dig, nw,
+                                [&](ge_p3& accB) {  // [k2 S]B (pv_straus_b_kernel)
+#pragma unroll
+                                    for (int q = 0; q < 10; q++) {
+                                        accB.X.v[q] = qs.ld(q, i);
+                                        accB.Y.v[q] = qs.ld(10 + q, i);
+                                        accB.Z.v[q] = qs.ld(20 + q, i);
+                                        accB.T.v[q] = qs.ld(30 + q, i);
+                                    }
+                                });
+#else
         const DevATab rt{wk.atab, (uint32_t)wk.stride, i, 9u};
         pv_straus_ar_xyz(X, Y, Z, at, rt, dig, nw, [&](ge_p3& accB) {  // [k2 S]B (pv_straus_b_kernel)
 #pragma unroll
@@ -626,6 +727,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
                 accB.T.v[q] = qs.ld(30 + q, i);
             }
         });
+#endif
 #elif PV_STRAUS_WIDE_B
         pv_straus_a_xyz(X, Y, Z, at, dig, [&](ge_p3& accB) {  // [S]B, written by pv_straus_b_kernel
 #pragma unroll
@@ -970,28 +1072,6 @@ struct DevBRows {
         return DevBRow{base + (uint32_t)i * PV_BCOMB_ENT * (PV_BCOMB_STRIDE / 4)};
     }
 };
-
-// LDS-DMA staging of one table entry per lane (comb.h, PV_COMB_PIPELINE). An entry of Q uint4 is
-// fetched by Q global_load_lds_dwordx4, each writing 1 KiB = 16 B x 64 lanes of the wave's staging
-// area, laid out [q][lane] so that reading it back is one conflict-free ds_read_b128 per q.
-__device__ __forceinline__ void pv_glds16(const uint4* g, uint4* l) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                     (__attribute__((address_space(3))) void*)l, 16, 0, 0);
-}
-// Q pieces of 16 B from g[0..Q) to l[q * 64 + lane] (a wave's [q][lane] staging area). The
-// instruction's immediate offset (16 q) applies to BOTH the global and the LDS address, so the LDS
-// base of piece q is moved back by the same 16 q bytes (M0 is set per instruction anyway): all Q
-// loads then share ONE 64-bit global address instead of Q 64-bit adds per staged entry.
-template <int Q, int q = 0>
-__device__ __forceinline__ void pv_glds16_row(const uint4* g, uint4* l) {
-    if constexpr (q < Q) {
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                         (__attribute__((address_space(3))) void*)(l + q * 64 - q), 16, 16 * q, 0);
-        pv_glds16_row<Q, q + 1>(g, l);
-    }
-}
-// the LDS reads of the previous staged entry must be complete before its buffer is refilled
-__device__ __forceinline__ void pv_lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 struct DevCombStage {  // per-key comb table rows, entries of 10 uint4
     const uint4* key;  // the key's table [32][129][10]
@@ -1945,6 +2025,10 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_LAUNCH_BC2(pv_prep_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#if PV_STRAUS_HALF
+            PV_LAUNCH_BC2(pv_split_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m, g_ctx.work, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#endif
             hipLaunchKernelGGL(pv_table_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m, d_pk + 32 * c0,
                                g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -1982,6 +2066,10 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_LAUNCH_BC2(pv_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                                d_pk + 32 * c0, g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#if PV_STRAUS_HALF
+            PV_LAUNCH_BC2(pv_split_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m, g_ctx.work, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#endif
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
             hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m, d_pk + 32 * c0,
                                g_ctx.work, gate);

@@ -137,13 +137,28 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
             __syncthreads();  // 2: [S]B is ready
             return;
         }
-        uint32_t k[8];
+        uint32_t k[8], S[8];
         pv_hash_k(k, in, smlen, mw);
         LAT_STAMP(9);
+        // every lane holds the same k: made uniform, the split runs on the scalar unit (short
+        // dependent-instruction latency: this is one wave's serial chain)
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            k[q] = __builtin_amdgcn_readfirstlane(k[q]);
+            S[q] = __builtin_amdgcn_readfirstlane(in.S[q]);
+        }
         pv_halfk hk;
+#ifdef PV_LAT_TRACE
+        uint32_t st[3] = {0, 0, 0};
+        sc_halfsize(hk, k, st);
+        if (blockIdx.x == 0 && lane == 0) pv_lat_trace_buf[15] = st[0] | (st[1] << 8) | ((uint64_t)st[2] << 16);
+#else
         sc_halfsize(hk, k);
+#endif
+        LAT_STAMP(12);
         uint32_t s2[8], fs[8], e1[8], e2[8];
-        sc_mul(s2, hk.k2, in.S);
+        sc_mul(s2, hk.k2, S);
+        LAT_STAMP(13);
         sc_recode65536(fs, s2);
         lu ent[PV_BCOMB_POS];
 #pragma unroll
@@ -222,6 +237,207 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 #endif
 }
 
+// Four-wave form for small batches (PV_LAT4_MAX): each of [k1](+-A) and [k2](-R') is split once more at
+// window PV_LAT4_SPLIT (2^68), k_i = lo + 2^68 hi, so four waves run ~17 windows each at the same time:
+//   wave 0  decompression of A and R (one chain), -A and R' published (LDS flag), tables of -A and R';
+//           then lo(k1) on -A
+//   wave 1  checks, k, the split, s2 = k2 S mod L and its comb entries; then lo(k2) on -R' + [s2]B
+//   wave 2  waits for -A, doubles it 68 times, table of [2^68](-A); then hi(k1) on it
+//   wave 3  the same for R': table of [2^68]R'; then hi(k2) on its negation
+//   wave 0  sums the four parts, + R', compares with R' (lp_final_check).
+// A cached key keeps the two-wave cached flow (waves 2 and 3 only join the barriers).
+#ifndef PV_LAT4_MAX
+#define PV_LAT4_MAX 256  // batches up to this size take the four-wave form (more waves, less chain)
+#endif
+#ifndef PV_LAT4_SPLIT
+#define PV_LAT4_SPLIT 17
+#endif
+constexpr int LAT4_THREADS = 256;
+
+__global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __restrict__ sm,
+                                                               const uint64_t* __restrict__ off, uint64_t n,
+                                                               const uint8_t* __restrict__ pk,
+                                                               const uint32_t* __restrict__ bcomb, PvKeyCacheView kc,
+                                                               unsigned long long* __restrict__ verdict,
+                                                               const uint32_t* __restrict__ run_if) {
+#if LP_DEVICE
+    if (run_if && *run_if == 0u) return;
+    const uint32_t r = blockIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    __shared__ uint32_t s_k1[8], s_k2[8];   // signed radix-16 digits of |k1|, k2
+    __shared__ uint32_t s_k256[8];          // radix-256 digits of k (cached key)
+    __shared__ uint32_t s_sig_ok, s_nw, s_neg;
+    __shared__ volatile uint32_t s_pts_ready;  // wave 0 -> waves 2, 3: -A and R' published
+    __shared__ uint32_t s_pa[64], s_pr[64];    // -A, R' (ext)
+    __shared__ uint32_t s_part[3][64];         // wave 1, 2, 3 results (ext)
+    __shared__ uint32_t s_tab[4][17][64];      // [j] of -A, R', [2^68](-A), [2^68]R', j = -8..8
+
+    if (threadIdx.x == 0) s_pts_ready = 0u;
+    const uint64_t o0 = off[r], o1 = off[r + 1];
+    const uint64_t smlen = o1 - o0;
+    const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
+    const LatMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+    pv_sig_words in;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        in.R[q] = mw.dw(q);
+        in.S[q] = mw.dw(8 + q);
+    }
+    {
+        const uint4* p4 = reinterpret_cast<const uint4*>(pk + 32 * (uint64_t)r);
+        const uint4 a0 = p4[0], a1 = p4[1];
+        in.A[0] = a0.x; in.A[1] = a0.y; in.A[2] = a0.z; in.A[3] = a0.w;
+        in.A[4] = a1.x; in.A[5] = a1.y; in.A[6] = a1.z; in.A[7] = a1.w;
+    }
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(pv_kc_lookup(kc, in.A));
+    const bool cached = slot != PV_KC_EMPTY;
+    __syncthreads();  // 0: s_pts_ready cleared
+    LAT_STAMP(wave == 0 ? 0 : (wave == 1 ? 8 : 14));
+
+    if (wave >= 2) {
+        if (!cached) {
+            // wait for wave 0's decompression (a workgroup's waves are co-resident: it progresses)
+            while (s_pts_ready == 0u) __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            lu P = wave == 2 ? lu(s_pa[lane]) : lu(s_pr[lane]);
+            for (int j = 0; j < 4 * PV_LAT4_SPLIT; j++) P = lp_dbl(c, P);
+            lp_build_a_table(c, K, P, [&](int j, const lu& q) { s_tab[wave][j + 8][lane] = q; });
+        }
+        __syncthreads();  // 1: split, tables ready
+        if (!cached) {
+            const int nw = __builtin_amdgcn_readfirstlane((int)s_nw);
+            const int sgn = wave == 3 ? -1 : (s_neg ? -1 : 1);  // k2's part goes on -R''
+            const uint32_t* dg = wave == 2 ? s_k1 : s_k2;
+            s_part[wave - 1][lane] = lp_straus_range(c, PV_LAT4_SPLIT, nw, [&](int i) { return sgn * pv_nibble(dg[i >> 3], i); },
+                                                     [&](int e) -> lu { return s_tab[wave][e + 8][lane]; });
+        }
+        __syncthreads();  // 2
+        return;
+    }
+    if (wave == 1) {
+        const bool sig_ok = pv_sig_ok(in, smlen);
+        if (cached) {
+            uint32_t fs[8];
+            sc_recode65536(fs, in.S);
+            lu ent[PV_BCOMB_POS];
+#pragma unroll
+            for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
+            uint32_t k[8], e256[8];
+            pv_hash_k(k, in, smlen, mw);
+            sc_recode256(e256, k);
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) s_k256[q] = e256[q];
+                s_sig_ok = sig_ok ? 1u : 0u;
+            }
+            __syncthreads();  // 1
+            s_part[0][lane] = lp_comb_b(c, [&](int j) -> lu { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); });
+            __syncthreads();  // 2
+            return;
+        }
+        uint32_t k[8], S[8];
+        pv_hash_k(k, in, smlen, mw);
+        LAT_STAMP(9);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            k[q] = __builtin_amdgcn_readfirstlane(k[q]);
+            S[q] = __builtin_amdgcn_readfirstlane(in.S[q]);
+        }
+        pv_halfk hk;
+        sc_halfsize(hk, k);
+        LAT_STAMP(12);
+        uint32_t s2[8], fs[8], e1[8], e2[8];
+        sc_mul(s2, hk.k2, S);
+        sc_recode65536(fs, s2);
+        lu ent[PV_BCOMB_POS];
+#pragma unroll
+        for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
+        sc_recode16(e1, hk.k1);
+        sc_recode16(e2, hk.k2);
+        const int nw1 = sc_nwin16(e1), nw2 = sc_nwin16(e2);
+        const int nw = __builtin_amdgcn_readfirstlane(nw1 > nw2 ? nw1 : nw2);
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                s_k1[q] = e1[q];
+                s_k2[q] = e2[q];
+            }
+            s_nw = (uint32_t)nw;
+            s_neg = hk.neg ? 1u : 0u;
+            s_sig_ok = sig_ok ? 1u : 0u;
+        }
+        LAT_STAMP(10);
+        __syncthreads();  // 1
+        const int hi = nw < PV_LAT4_SPLIT ? nw : PV_LAT4_SPLIT;
+        lu acc = lp_straus_range(c, 0, hi, [&](int i) { return -pv_nibble(e2[i >> 3], i); },
+                                 [&](int e) -> lu { return s_tab[1][e + 8][lane]; });
+#pragma unroll
+        for (int j = PV_BCOMB_POS - 1; j >= 0; j--) acc = lp_add_cached(c, acc, lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)));
+        s_part[0][lane] = acc;
+        LAT_STAMP(11);
+        __syncthreads();  // 2
+        return;
+    }
+    // wave 0
+    lu sw[8];
+    const lm odd_row = lp_eq(c.row & 1u, 1u);
+#pragma unroll
+    for (int q = 0; q < 8; q++) sw[q] = lp_sel(odd_row, in.R[q], in.A[q]);
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    LAT_STAMP(1);
+    const bool r_ok = pv_ge_is_canonical(in.R) && dec.ok_r && !(dec.x_r_zero && (in.R[7] >> 31));
+    bool key_ok;
+    lu QA;
+    if (cached) {
+        key_ok = kc.flags[slot] != 0;
+        const uint32_t* tab = reinterpret_cast<const uint32_t*>(kc.tab + (uint64_t)slot * PV_COMB_POS * PV_COMB_ENT * 10);
+        __syncthreads();  // 1
+        uint32_t e256[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) e256[q] = s_k256[q];
+        lu ent[PV_COMB_POS];
+#pragma unroll
+        for (int i = 0; i < PV_COMB_POS; i++) ent[i] = lp_ctab_load(c, tab, i, pv_byte(e256[i >> 2], i));
+        QA = lp_comb_a(c, [&](int i) { return lp_ctab_fix(c, ent[i], pv_byte(e256[i >> 2], i)); });
+        __syncthreads();  // 2
+    } else {
+        key_ok = pv_ge_is_canonical(in.A) && !pv_has_small_order(in.A) && dec.ok_a;
+        const lu negA = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);
+        const lu Rp = lp_ext_from_xy(c, K, dec.X, dec.Y, 1);
+        s_pa[lane] = negA;
+        s_pr[lane] = Rp;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) s_pts_ready = 1u;
+        lp_build_a_table(c, K, negA, [&](int j, const lu& q) { s_tab[0][j + 8][lane] = q; });
+        lp_build_a_table(c, K, Rp, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });
+        LAT_STAMP(2);
+        __syncthreads();  // 1
+        LAT_STAMP(3);
+        const int nw = __builtin_amdgcn_readfirstlane((int)s_nw);
+        const int sgn = s_neg ? -1 : 1;
+        const int hi = nw < PV_LAT4_SPLIT ? nw : PV_LAT4_SPLIT;
+        QA = lp_straus_range(c, 0, hi, [&](int i) { return sgn * pv_nibble(s_k1[i >> 3], i); },
+                             [&](int e) -> lu { return s_tab[0][e + 8][lane]; });
+        QA = lp_add_cached(c, QA, s_tab[1][9][lane]);  // + R'
+        LAT_STAMP(4);
+        __syncthreads();  // 2
+        LAT_STAMP(5);
+        // + the hi parts of k1 and k2 (waves 2, 3); wave 1's part is added by lp_final_check
+        QA = lp_add_cached(c, QA, lp_to_cached(c, lu(s_part[1][lane]), K.d2));
+        QA = lp_add_cached(c, QA, lp_to_cached(c, lu(s_part[2][lane]), K.d2));
+    }
+    // cached: QA = [k](-A), wave 1's part [S]B; otherwise QA = [k1](+-A) + R' + [2^68 hi(k2)](-R'), wave
+    // 1's part [lo(k2)](-R') + [s2]B
+    const bool eq = lp_final_check(c, K, QA, s_part[0][lane], dec.X, dec.Y);
+    const bool ok = eq && key_ok && r_ok && s_sig_ok != 0;
+    if (lane == 0 && ok) atomicOr(&verdict[r >> 6], 1ull << (r & 63));
+    LAT_STAMP(6);
+#endif
+}
+
 }  // namespace
 
 #ifdef PV_LAT_TRACE
@@ -241,9 +457,14 @@ int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, co
         e = hipMemsetAsync(d_verdict, 0, (n + 63) / 64 * 8, stream);
         if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
     }
-    hipLaunchKernelGGL(pv_lat_kernel, dim3((unsigned)n), dim3(LAT_THREADS), 0, stream, d_sm, d_off, n, d_pk,
-                       reinterpret_cast<const uint32_t*>(d_bcomb), kc, reinterpret_cast<unsigned long long*>(d_verdict),
-                       run_if);
+    if (n <= PV_LAT4_MAX)
+        hipLaunchKernelGGL(pv_lat4_kernel, dim3((unsigned)n), dim3(LAT4_THREADS), 0, stream, d_sm, d_off, n, d_pk,
+                           reinterpret_cast<const uint32_t*>(d_bcomb), kc,
+                           reinterpret_cast<unsigned long long*>(d_verdict), run_if);
+    else
+        hipLaunchKernelGGL(pv_lat_kernel, dim3((unsigned)n), dim3(LAT_THREADS), 0, stream, d_sm, d_off, n, d_pk,
+                           reinterpret_cast<const uint32_t*>(d_bcomb), kc,
+                           reinterpret_cast<unsigned long long*>(d_verdict), run_if);
     e = hipGetLastError();
     if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("pv_lat_kernel: ") + hipGetErrorString(e));
     return PV_OK;

@@ -184,9 +184,10 @@ PV_HD void sc_recode65536(uint32_t out[8], const uint32_t a[8]) {
 //
 // sc_halfsize: the extended Euclidean algorithm on (8L, k) -- remainders r_i = k t_i (mod 8L), t_0 = 0,
 // t_1 = 1 -- stopped at the first r_i < 2^128 whose t_i is odd. While r_i >= 2^131 the steps are taken
-// in Lehmer blocks (Knuth, TAOCP 4.5.2, Algorithm L): ~15 quotients at a time from the leading 52 bits
-// of the pair in double precision (each accepted only when both bracketing quotients agree), then ONE
-// multiword update of (r, t) by the block's 2x2 matrix; the last few bits go by exact single steps
+// in Lehmer blocks (Knuth, TAOCP 4.5.2, Algorithm L): ~9 quotients at a time from the leading 31 bits
+// of the pair (single-precision reciprocal estimates fixed in integer arithmetic; a quotient is
+// accepted only when both of Knuth's bracketing quotients agree), then ONE multiword update of (r, t)
+// by the block's 2x2 matrix; the last few bits go by exact single steps
 // (a double-precision quotient estimate corrected in exact multiword arithmetic). Every update applies
 // the same integer matrix to r and to t (t in two's complement), so r_i = k t_i (mod 8L) holds whatever
 // the quotients were; a step whose estimate cannot be settled (a quotient >= 2^32, |t| >= 2^168,
@@ -198,7 +199,7 @@ static constexpr uint32_t SC_8L[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa
 #define PV_HALF_MAXIT 64  // exact single steps (after the Lehmer blocks: ~3-12)
 #endif
 #ifndef PV_HALF_BLOCKS
-#define PV_HALF_BLOCKS 16  // Lehmer blocks (~5-6 needed from 2^255 to 2^131)
+#define PV_HALF_BLOCKS 24  // Lehmer blocks (~9 needed from 2^255 to 2^131)
 #endif
 struct pv_halfk {
     uint32_t k1[8];  // |k1|
@@ -280,15 +281,34 @@ PV_HD bool mp_small168(const uint32_t t[8]) {
     return t[7] == s && t[6] == s && ((t[5] ^ s) >> 8) == 0;
 }
 
-// floor(a / b) for 0 <= a < 2^53, 0 < b < 2^53 (exact: double estimate, integer fix-up)
-PV_HD int64_t pv_fdiv53(int64_t a, int64_t b) {
-    int64_t q = (int64_t)((double)a / (double)b);
-    if (q * b > a) q--;
-    else if ((q + 1) * b <= a) q++;
+// floor(n / d) for 0 <= n < 2^31, 0 < d < 2^31 from a single-precision reciprocal estimate, fixed by
+// one exact step each way; ok = false (the caller ends its Lehmer block) for n < 0, d <= 0, a
+// quotient >= 2^20 or an estimate one step could not fix
+PV_HD uint32_t pv_qdiv31(int32_t n, int32_t d, bool& ok) {
+    ok = n >= 0 && d > 0;
+    const uint32_t un = ok ? (uint32_t)n : 0u, ud = ok ? (uint32_t)d : 1u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float qf = (float)un * __builtin_amdgcn_rcpf((float)ud);
+#else
+    const float qf = (float)un / (float)ud;
+#endif
+    uint32_t q = qf < 1048576.0f ? (uint32_t)qf : 1048576u;
+    uint64_t p = (uint64_t)q * ud;
+    if (p > un) {
+        q--;
+        p -= ud;
+    }
+    if (p + ud <= un) {
+        q++;
+        p += ud;
+    }
+    ok = ok && q < 1048576u && p <= un && p + ud > un;
     return q;
 }
 
-PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8]) {
+// stats (measurement only, nullptr otherwise): [0] Lehmer blocks, [1] quotients settled inside them,
+// [2] exact single steps
+PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8], uint32_t* stats = nullptr) {
     uint32_t r0[9], r1[9], t0[8], t1[8];  // r: 9 words (word 8 = 0 for a valid state)
 #pragma unroll
     for (int i = 0; i < 9; i++) {
@@ -306,7 +326,7 @@ PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8]) {
         const bool act = !bad && ((r1[4] >> 3) | r1[5] | r1[6] | r1[7]) != 0;
         if (pv_wave_all(!act)) break;
         if (!act) continue;
-        // leading bits: xh = floor(r0 / 2^e), yh = floor(r1 / 2^e), xh < 2^52 (r0 >= 2^131: w >= 4)
+        // leading bits: xh = floor(r0 / 2^e), yh = floor(r1 / 2^e), 2^30 <= xh < 2^31 (r0 >= 2^131: w >= 4)
         int w = 4;
 #pragma unroll
         for (int i = 5; i < 8; i++) w = r0[i] ? i : w;
@@ -318,36 +338,41 @@ PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8]) {
             b1 = i == w ? r1[i] : b1;
             b0 = i == w ? r1[i - 1] : b0;
         }
-        const int sh = 12 - (int)__builtin_clz(a1);  // bits above 52 in (a1:a0)
-        const int s = sh > 0 ? sh : 0;
-        const int64_t xh0 = (int64_t)((((uint64_t)a1 << 32) | a0) >> s);
-        const int64_t yh0 = (int64_t)((((uint64_t)b1 << 32) | b0) >> s);
-        // stop a block above 2^130: yh < 2^(130 - e), e = 32 (w - 1) + s (>= 79 here)
+        const int s = 33 - (int)__builtin_clz(a1);  // (a1:a0) has 64 - clz bits; keep the top 31
+        const int32_t xh0 = (int32_t)((((uint64_t)a1 << 32) | a0) >> s);
+        const int32_t yh0 = (int32_t)((((uint64_t)b1 << 32) | b0) >> s);
+        // stop a block above 2^130: yh < 2^(130 - e), e = 32 (w - 1) + s (>= 100 here)
         const int e = 32 * (w - 1) + s;
-        const int64_t ythr = e >= 130 ? 1 : ((int64_t)1 << (130 - e));
-        int64_t xh = xh0, yh = yh0, A = 1, B = 0, C = 0, D = 1;
+        const int32_t ythr = e >= 130 ? 1 : (int32_t)(1u << (130 - e));
+        int32_t xh = xh0, yh = yh0, A = 1, B = 0, C = 0, D = 1;
         bool go = true;
-        for (int it = 0; it < 40; it++) {
+        for (int it = 0; it < 24; it++) {
             if (pv_wave_all(!go)) break;
             if (!go) continue;
-            if (yh + C <= 0 || yh + D <= 0 || xh + A < 0 || xh + B < 0) {
+            // Knuth's test: the quotient of (xh + A) / (yh + C) and of (xh + B) / (yh + D) agree
+            const int32_t n1 = xh + A, d1 = yh + C, n2 = xh + B, d2 = yh + D;
+            bool ok1, ok2;
+            const uint32_t q = pv_qdiv31(n1, d1, ok1);
+            const uint32_t q2 = pv_qdiv31(n2, d2, ok2);
+            if (!ok1 || !ok2 || q != q2) {
                 go = false;
                 continue;
             }
-            const int64_t q = pv_fdiv53(xh + A, yh + C);
-            if (q != pv_fdiv53(xh + B, yh + D)) { go = false; continue; }
-            const int64_t ny = xh - q * yh, nC = A - q * C, nD = B - q * D;
-            if (ny < ythr || nC >= 0x7FFFFFFF || nC <= -0x7FFFFFFF || nD >= 0x7FFFFFFF || nD <= -0x7FFFFFFF) {
+            const int64_t ny = (int64_t)xh - (int64_t)q * yh;
+            const int64_t nC = (int64_t)A - (int64_t)q * C, nD = (int64_t)B - (int64_t)q * D;
+            if (ny < ythr || nC >= 32768 || nC <= -32768 || nD >= 32768 || nD <= -32768) {
                 go = false;
                 continue;
             }
             A = C;
-            C = nC;
+            C = (int32_t)nC;
             B = D;
-            D = nD;
+            D = (int32_t)nD;
             xh = yh;
-            yh = ny;
+            yh = (int32_t)ny;
+            if (stats) stats[1]++;
         }
+        if (stats) stats[0]++;
         if (B == 0) {
             // no quotient could be settled from the leading bits: one exact step below
             // (the block loop then continues from the new pair)
@@ -381,7 +406,7 @@ PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8]) {
             }
         } else {
             uint32_t u[9], v[9], nr0[9], nr1[9], nt0[8], nt1[8], x[8], y[8];
-            mp_muls32<9>(u, r0, A);
+            mp_muls32<9>(u, r0, A);  // |A|, |B|, |C|, |D| < 2^15
             mp_muls32<9>(v, r1, B);
             mp_add<9>(nr0, u, v);
             mp_muls32<9>(u, r0, C);
@@ -412,6 +437,7 @@ PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8]) {
     for (int it = 0; it < PV_HALF_MAXIT; it++) {
         if (pv_wave_all(done || bad)) break;
         if (done || bad) continue;
+        if (stats) stats[2]++;
         const double qd = sc_to_double(r0) / sc_to_double(r1);  // r1 = 0: +inf -> bad
         bad |= !(qd < 4294967295.0);
         uint32_t q = bad ? 0u : (uint32_t)qd;

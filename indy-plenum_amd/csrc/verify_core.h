@@ -281,6 +281,96 @@ PV_HD void pv_straus_ar_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const RTab& r
     ge_p1p1_to_p2(X, Y, Z, t);
 }
 
+// The same loop with the table entries software-pipelined (as comb.h pv_comb_a_xyz_staged): st.stage(t,
+// j) starts fetching entry j of table t (0: [j](+-A), 1: [j](-R')) into the lane's staging buffer (on
+// the device LDS-DMA: no VGPRs held while in flight), st.staged(h, w) reads half h of it back. Each
+// addition starts the NEXT addition's fetch once it has read its own entry: R_w's during A_w's last
+// products, A_(w-1)'s during R_w's and the next window's four doublings.
+template <class St>
+PV_HD void pv_ar_step(ge_p1p1& r, const ge_p3& p, const St& st, int e, bool next, int nt, int ne) {
+    const bool neg = e < 0;
+    uint32_t w[20];
+    st.staged(0, w);
+    fe ypx, ymx, t, a, b, c, d, z2, t2d;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        ypx.v[i] = neg ? w[10 + i] : w[i];
+        ymx.v[i] = neg ? w[i] : w[10 + i];
+    }
+    fe_sub(t, p.Y, p.X);
+    fe_mul(a, t, ymx);
+    fe_add(t, p.Y, p.X);
+    fe_mul(b, t, ypx);
+    st.staged(1, w);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        z2.v[i] = w[i];
+        t2d.v[i] = w[10 + i];
+    }
+    if (next) st.stage(nt, ne < 0 ? -ne : ne);
+    fe_cneg(t2d, t2d, neg);
+    fe_mul(c, p.T, t2d);
+    fe_mul(d, p.Z, z2);
+    fe_sub(r.X, b, a);
+    fe_add(r.Y, b, a);
+    fe_add(r.Z, d, c);
+    fe_sub(r.T, d, c);
+}
+template <class St, class Dig, class AccB>
+PV_HD void pv_straus_ar_xyz_staged(fe& X, fe& Y, fe& Z, const St& st, const Dig& dig, int nw, const AccB& load_accB) {
+    ge_p3 acc;
+    ge_p3_identity(acc);
+    ge_p1p1 t;
+    uint32_t w1 = dig.ek((nw - 1) >> 3), w2 = dig.ek2((nw - 1) >> 3);
+    int e1 = pv_nibble(w1, nw - 1), e2 = pv_nibble(w2, nw - 1);
+    st.stage(0, e1 < 0 ? -e1 : e1);
+    for (int win = nw - 1; win >= 0; win--) {
+        if (win != nw - 1) {
+            for (int j = 0; j < 3; j++) {
+                ge_p2_dbl(t, X, Y, Z);
+                ge_p1p1_to_p2(X, Y, Z, t);
+            }
+            ge_p2_dbl(t, X, Y, Z);
+            ge_p1p1_to_p3(acc, t);
+        }
+        pv_ar_step(t, acc, st, e1, true, 1, e2);
+        ge_p1p1_to_p3(acc, t);
+        // the next window's digits (a new word every 8 windows), then R_w with A_(win-1)'s fetch
+        int n1 = 0, n2 = 0;
+        if (win > 0) {
+            if ((win & 7) == 0) {
+                w1 = dig.ek((win - 1) >> 3);
+                w2 = dig.ek2((win - 1) >> 3);
+            }
+            n1 = pv_nibble(w1, win - 1);
+            n2 = pv_nibble(w2, win - 1);
+        }
+        pv_ar_step(t, acc, st, e2, win > 0, 0, n1);
+        if (win > 0) ge_p1p1_to_p2(X, Y, Z, t);
+        e1 = n1;
+        e2 = n2;
+    }
+    ge_p1p1_to_p3(acc, t);
+    ge_p3 accB;
+    load_accB(accB);
+    ge_cached cb;
+    ge_p3_to_cached(cb, accB);
+    ge_add_cached(t, acc, cb);
+    ge_p1p1_to_p3(acc, t);
+    st.stage(1, 1);  // + R'
+    pv_ar_step(t, acc, st, -1, false, 0, 0);
+    ge_p1p1_to_p2(X, Y, Z, t);
+}
+// Staging over two plain table objects (host tests): stage() remembers the entry, staged() reads it.
+template <class ATab>
+struct PvTabStage2 {
+    const ATab& a;
+    const ATab& r;
+    mutable int t, j;
+    PV_HD void stage(int tab, int ent) const { t = tab; j = ent; }
+    PV_HD void staged(int h, uint32_t w[20]) const { (t ? r : a).load_half(j, h, w); }
+};
+
 template <class ATab, class BTab, class Dig>
 PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const Dig& dig) {
     fe X, Y, Z;

@@ -362,10 +362,14 @@ int hc_sign_open_straus_half16(const uint8_t* sm, uint64_t smlen, const uint8_t*
     HostBRows brows{bcomb.data()};
     ge_p3 accB;
     pv_comb_b_acc_w<16>(accB, PvRowsStageB<HostBRows>{brows, 0, 0}, [&](int j) { return fb[j]; });
-    fe X, Y, Z;
+    fe X, Y, Z, X2, Y2, Z2;
     pv_straus_ar_xyz(X, Y, Z, at, rt, dig, nw, [&](ge_p3& p) { p = accB; });
-    uint32_t enc[8];
+    // the LDS-staged loop the device runs (pv_straus_ar_xyz_staged) gives the same point
+    pv_straus_ar_xyz_staged(X2, Y2, Z2, PvTabStage2<HostATab>{at, rt, 0, 0}, dig, nw, [&](ge_p3& p) { p = accB; });
+    uint32_t enc[8], enc2[8];
     ge_p2_tobytes(enc, X, Y, Z);
+    ge_p2_tobytes(enc2, X2, Y2, Z2);
+    if (!pv_words_equal(enc, enc2)) return -1;
     return ok && pv_words_equal(enc, in.R);
 }
 
@@ -509,6 +513,63 @@ int hc_lp_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     const lu QA = lp_add_cached(c, lp_straus_nw(c, nw, [&](int i) { return sgn * pv_nibble(e1[i >> 3], i); },
                                                 [&](int e) { return tab[e + 8]; }),
                                 rtab[9]);
+    const bool eq = lp_final_check(c, K, QA, SB, dec.X, dec.Y);
+    return eq && key_ok && r_ok && sig_ok;
+}
+
+// The four-wave form (pv_lat4_kernel): [k1](+-A) and [k2](-R') each split at window `split`, the high
+// parts on tables of [2^(4 split)](-A) and [2^(4 split)]R' (4 split doublings each), summed as wave 0
+// sums them, then lp_final_check against R'.
+int hc_lp4_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk, int split) {
+    const std::vector<uint32_t>& bcomb = host_bcomb();
+    std::vector<uint8_t> buf(smlen + 256, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    HostMsg mw{buf.data()};
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    const bool sig_ok = pv_sig_ok(in, smlen);
+    uint32_t k[8];
+    pv_hash_k(k, in, smlen, mw);
+    pv_halfk hk;
+    sc_halfsize(hk, k);
+    uint32_t s2[8], fs[8], e1[8], e2[8];
+    sc_mul(s2, hk.k2, in.S);
+    sc_recode65536(fs, s2);
+    sc_recode16(e1, hk.k1);
+    sc_recode16(e2, hk.k2);
+    const int nw = std::max(sc_nwin16(e1), sc_nwin16(e2));
+    lu sw[8];
+    const lm odd_row = lp_eq(c.row & 1u, 1u);
+    for (int q = 0; q < 8; q++) sw[q] = lp_sel(odd_row, in.R[q], in.A[q]);
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    const bool key_ok = pv_ge_is_canonical(in.A) && !pv_has_small_order(in.A) && dec.ok_a;
+    const bool r_ok = pv_ge_is_canonical(in.R) && dec.ok_r && !(dec.x_r_zero && (in.R[7] >> 31));
+    const lu negA = lp_ext_from_xy(c, K, dec.X, dec.Y, 0), Rp = lp_ext_from_xy(c, K, dec.X, dec.Y, 1);
+    std::vector<lu> tab[4];
+    lu base[4] = {negA, Rp, negA, Rp};
+    for (int w = 2; w < 4; w++)
+        for (int j = 0; j < 4 * split; j++) base[w] = lp_dbl(c, base[w]);
+    for (int w = 0; w < 4; w++) {
+        tab[w].resize(17);
+        lp_build_a_table(c, K, base[w], [&](int j, const lu& q) { tab[w][j + 8] = q; });
+    }
+    const int sgn = hk.neg ? -1 : 1;
+    const int hi = std::min(nw, split);
+    auto d1 = [&](int i) { return sgn * pv_nibble(e1[i >> 3], i); };
+    auto d2 = [&](int i) { return -pv_nibble(e2[i >> 3], i); };
+    lu SB = lp_straus_range(c, 0, hi, d2, [&](int e) { return tab[1][e + 8]; });
+    for (int j = PV_BCOMB_POS - 1; j >= 0; j--)
+        SB = lp_add_cached(c, SB, lp_bcomb_fix(c, lp_bcomb_entry(c, bcomb.data(), j, pv_half(fs[j >> 1], j)), pv_half(fs[j >> 1], j)));
+    const lu p2 = lp_straus_range(c, split, nw, d1, [&](int e) { return tab[2][e + 8]; });
+    const lu p3 = lp_straus_range(c, split, nw, d2, [&](int e) { return tab[3][e + 8]; });
+    lu QA = lp_straus_range(c, 0, hi, d1, [&](int e) { return tab[0][e + 8]; });
+    QA = lp_add_cached(c, QA, tab[1][9]);
+    QA = lp_add_cached(c, QA, lp_to_cached(c, p2, K.d2));
+    QA = lp_add_cached(c, QA, lp_to_cached(c, p3, K.d2));
     const bool eq = lp_final_check(c, K, QA, SB, dec.X, dec.Y);
     return eq && key_ok && r_ok && sig_ok;
 }

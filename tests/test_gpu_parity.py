@@ -37,6 +37,19 @@ def test_each_adversarial_class(native, sodium, oracle):
     assert want.sum() > 24 * 3
 
 
+def test_each_adversarial_class_small_batches(native, sodium, oracle):
+    """Per class, a batch of 16 (at or below PV_LAT4_MAX: the latency path's four-wave form, where
+    [k1](+-A) and [k2](-R') are each cut at 2^68; the other paths run their usual kernels), mixed-order
+    A and R with passing and failing signatures included."""
+    g = VectorGen(sodium, oracle, seed=12)
+    for cls in VectorGen.CLASSES:
+        cases = [g.make(cls) for _ in range(16)]
+        blob, off, pks = pack(cases)
+        got = native.verify_sm_batch(blob, off, pks)
+        want = reference_verdicts(sodium, cases)
+        assert np.array_equal(got, want), (cls, np.nonzero(got != want)[0][:5])
+
+
 def test_mixed_batch_2pct(native, sodium, oracle):
     g = VectorGen(sodium, oracle, seed=12)
     cases = g.batch(3000, adversarial_frac=0.02)

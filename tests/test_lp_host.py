@@ -179,3 +179,25 @@ def test_lp_key_chain_in_parts(hc, oracle):
     for pk in keys:
         for parts in (1, 2, 4, 8):
             assert hc.hc_lp_chain_parts_check(pk, parts) == 0, parts
+
+
+def test_lp4_path_vs_libsodium(hc, sodium, oracle):
+    """The four-wave latency form (pv_lat4_kernel's arithmetic: the half-size split, each scalar cut
+    at window 17 with the high part on [2^68]-multiples) against golden verdicts of every class and
+    libsodium on every adversarial class, mixed-order A and R included; split points 1 and 40 too
+    (one scalar part empty / a split beyond the window count)."""
+    from vectors import VectorGen
+    with open(os.path.join(HERE, "golden", "verdicts.json")) as f:
+        cases = json.load(f)
+    seen = {}
+    for c in cases:
+        seen.setdefault((c["cls"], c["ok"]), []).append(c)
+    for key, cs in sorted(seen.items()):
+        c = cs[0]
+        sm, pk = bytes.fromhex(c["sm"]), bytes.fromhex(c["pk"])
+        assert bool(hc.hc_lp4_sign_open(sm, ctypes.c_uint64(len(sm)), pk, 17)) == c["ok"], key
+    g = VectorGen(sodium, oracle, seed=29)
+    for cls in VectorGen.CLASSES:
+        for split in (17, 1, 40):
+            sm, pk = g.make(cls)
+            assert bool(hc.hc_lp4_sign_open(sm, ctypes.c_uint64(len(sm)), pk, split)) == sodium.sign_open_ok(sm, pk), (cls, split)

@@ -5,7 +5,8 @@ with PLENUM_AMD_LIB. Verifies a 1-request batch `reps` times on the forced laten
 for the last call, block 0's s_memrealtime stamps (100 MHz) relative to wave 0's start, in us:
   wave 0: 0 start, 1 decompression done, 2 tables done, 3 past barrier 1, 4 loop done,
           5 past barrier 2, 6 verdict written
-  wave 1: 8 start, 9 k ready, 10 split ready (half-size), 11 [S]B / [k2](-R') + [s2]B done
+  wave 1: 8 start, 9 k ready, 12 split done, 13 k2 S mod L done, 10 digits and comb entries ready,
+          11 [S]B / [k2](-R') + [s2]B done
 """
 import ctypes
 import json
@@ -34,10 +35,11 @@ def main():
         buf = (ctypes.c_ulonglong * 16)()
         assert L.pv_debug_lat_trace(buf) == 0
         t = list(buf)
-        runs.append({i: round((t[i] - t[0]) / 100.0, 2) for i in (0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11)})
+        runs.append({i: round((t[i] - t[0]) / 100.0, 2) for i in (0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14)})
+        stats = {"lehmer_blocks": t[15] & 255, "block_quotients": (t[15] >> 8) & 255, "exact_steps": t[15] >> 16}
     med = {i: float(np.median([r[i] for r in runs])) for i in runs[0]}
     print(json.dumps({"lib": os.environ.get("PLENUM_AMD_LIB", "default"), "ok": bool(got[0]),
-                      "median_us_from_wave0_start": med}))
+                      "median_us_from_wave0_start": med, "split_stats_last": stats}))
 
 
 if __name__ == "__main__":
