@@ -81,12 +81,13 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
  * stream at each stage boundary. pv_stage_times returns the device time (ms) of each stage summed
  * over all launches since then, in this order (PV_STAGE_*):
  *   KEYS    per-batch key deduplication and per-key expansion (keyed comb path only)
- *   PREP    per-request checks, SHA-512, reduction mod L, recoding (and decompression of A on the
- *           Straus path)
- *   TABLE   per-request [j](-A) multiples (Straus path) / comb path: [S]B from the fixed-base comb
- *           while the per-key comb tables are built on a second stream, then the join
- *   MSM     the double-scalar multiplication [S]B + [k](-A) to projective coordinates (comb path:
- *           the [k](-A) half, 32 table additions)
+ *   PREP    per-request checks, SHA-512, reduction mod L, recoding (Straus path: also A's
+ *           decompression and the half-size split of k, pv_split_kernel)
+ *   TABLE   per-request [j](+-A) and [j](-R') multiples with R's decompression, and [k2 S]B from the
+ *           wide fixed-base comb (Straus path) / comb path: [S]B from the fixed-base comb while the
+ *           per-key comb tables are built on a second stream, then the join
+ *   MSM     the double-scalar multiplication to projective coordinates (Straus path: ~33 windows of
+ *           both half-size scalars; comb path: the [k](-A) half, 32 table additions)
  *   ENCODE  batched inversion, canonical encoding, compare with R, verdict bits
  * and the number of launches (chunks). pv_kernel_times is the coarse three-way view
  * (KEYS+PREP, TABLE, MSM+ENCODE). pv_set_timing(0) stops recording. */
@@ -97,21 +98,29 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
 #define PV_STAGE_ENCODE 4
 #define PV_NSTAGES 5
 /* Arithmetic path for subsequent launches. Every path gives bit-identical verdicts:
- *   PV_PATH_STRAUS  per request: decompress A, 9-entry table of [j](-A), [S]B from the wide
- *                   fixed-base comb (11 radix-2^24 lookups: the top entry converted + 10 niels
- *                   additions), then a regular-window loop over k only: 63 x 4 doublings + 64
- *                   cached additions, and ONE final addition of [S]B
+ *   PV_PATH_STRAUS  per request: decompress A and R (R must decode to R' with encode(R') == R, else
+ *                   reject), split k = k1 / k2 (mod 8L) with |k1|, k2 < ~2^128 and k2 odd (extended
+ *                   Euclid in Lehmer blocks), 9-entry tables of [j](+-A) and [j](-R'), [k2 S mod L]B
+ *                   from the wide fixed-base comb (11 radix-2^24 lookups: the top entry converted +
+ *                   10 niels additions), then a regular-window loop over both scalars: ~33 x (4
+ *                   doublings + 2 cached additions), + [k2 S]B + R', and encode(.) == R: equal iff
+ *                   [k2](SB - kA - R') = 0 iff libsodium's encode(SB - kA) == R (any A, R of the
+ *                   curve: 8L kills every point, k2 is odd and below L). A lane whose split is not
+ *                   settled takes (k, 1) and the full-length loop, same verdict
  *   PV_PATH_COMB    per batch: deduplicate keys; per DISTINCT key: libsodium's key checks,
  *                   decompression and a radix-256 comb table T_A[i][d] = [d 256^i](-A) (32 x 129
  *                   entries); per request: [S]B as above (10 niels additions) and [k](-A) as 32
  *                   cached table additions, no doublings (keys beyond the PV_KEY_CAP = 16,384 tables
  *                   a chunk holds take the Straus path in the same launch)
- *   PV_PATH_LATENCY per request: one workgroup (two waves) with limb-parallel arithmetic, every
- *                   field element spread over 10 lanes of a 16-lane row; decompression of A and R in
- *                   one chain, [S]B from the radix-65536 fixed-base comb, [k](-A) by 252 doublings +
- *                   64 additions (32 table additions for a key in the node-side key cache), and the
- *                   comparison with R without an inversion. One kernel launch; the fastest path for
- *                   small batches (Plenum's 100 / 1,000-message quotas)
+ *   PV_PATH_LATENCY per request: one workgroup with limb-parallel arithmetic, every field element
+ *                   spread over 10 lanes of a 16-lane row; decompression of A and R in one chain,
+ *                   the same half-size split as the Straus path, [k1](+-A) and [k2](-R') (~33 x 4
+ *                   doublings + ~33 additions each) on two waves at once -- batches of <= 256
+ *                   requests: four waves, each scalar cut again at 2^68 (~17 windows per wave) --
+ *                   [k2 S]B from the radix-65536 fixed-base comb, and the comparison with R' without
+ *                   an inversion. A key in the node-side key cache keeps the full k: [k](-A) as 32
+ *                   table additions, no doublings. One kernel launch; the fastest path for small
+ *                   batches (Plenum's 100 / 1,000-message quotas)
  *   PV_PATH_AUTO    (default) batches of <= 2,048 requests take the latency path. From 2,049 to
  *                   4,096 requests AUTO picks by key repeats: the keyed path with >= 3 requests per
  *                   key (and <= 2,048 keys), else the latency path; pv_verify_batch counts the keys
@@ -144,7 +153,7 @@ int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* laun
  * of signers whose verkeys it already holds (the domain ledger's NYM records,
  * plenum/server/request_handlers/utils.py:30-39). For a cached key the latency path computes [k](-A)
  * with 32 additions from the key's radix-256 comb table (660 KB of HBM per key, built once by the
- * engine's key-chain and fill kernels) instead of 252 doublings + 64 additions; verdicts are
+ * engine's key-chain and fill kernels) instead of ~132 doublings + ~66 additions; verdicts are
  * unchanged (the table holds exact multiples of -A, and libsodium's key checks ran when it was built).
  * Above the latency path's range (AUTO: batches > 4,096 requests) a non-empty cache also makes every
  * chunk keyed, the tail chunk of a multi-chunk batch included: a cached key's requests take the comb

@@ -3,8 +3,9 @@ adversarial signatures"), SURVEY.md §8c (iv) classes.
 
 Every class keeps the record length, so the packed blob/offsets stay valid: bit flips in R/S/A/M,
 S + L, S in {L, L+1, 2^253-1, 2^256-1}, small-order R / A (with and without bit 255), non-canonical
-A, off-curve A, non-canonical R, and mixed-order keys A + T8 with an honest signature over the
-record's own message. The forger for the mixed-order class is libsodium 1.0.18 itself
+A, off-curve A, non-canonical R, mixed-order keys A + T8 with an honest signature over the
+record's own message, and mixed-order R' = rB + [j]T8 with S = r + k a under a prime-order key
+(never accepted) or under A + T8 (accepted iff [j]T8 = -[k]T8, about one in eight). The forger for the mixed-order class is libsodium 1.0.18 itself
 (crypto_scalarmult_ed25519_base_noclamp, crypto_core_ed25519_add, the reference's own native
 dependency) plus hashlib's SHA-512, so bench.py can build the batch without the test oracle; the
 tests pass the C oracle's forger instead (tests/adversarial.py). Seeded and deterministic.
@@ -29,7 +30,7 @@ BLACKLIST = [
 ORDER8 = BLACKLIST[2]
 
 CLASSES = ("flip_R", "flip_S", "flip_A", "flip_M", "S_plus_L", "S_big", "R_blacklist", "A_blacklist",
-           "A_noncanonical", "A_offcurve", "R_noncanonical", "mixed_order_A")
+           "A_noncanonical", "A_offcurve", "R_noncanonical", "mixed_order_A", "mixed_order_R", "mixed_order_AR")
 
 
 class SodiumForger:
@@ -89,6 +90,9 @@ def inject(blob, off, pks, frac, seed, forger=None):
     idx = np.sort(rng.choice(n, size=k, replace=False))
     labels = []
     offc = _offcurve_ys(rng, 64)
+    t8 = [ORDER8]  # [j]T8, j = 1..7
+    for _ in range(6):
+        t8.append(forger.point_add(t8[-1], ORDER8))
     for j, i in enumerate(idx):
         cls = CLASSES[j % len(CLASSES)]
         labels.append(cls)
@@ -137,6 +141,17 @@ def inject(blob, off, pks, frac, seed, forger=None):
             s2 = forger.sign_raw(r, a.to_bytes(32, "little"), A2, msg)
             sig[:] = np.frombuffer(s2, np.uint8)
             pks[i] = np.frombuffer(A2, np.uint8)
+        elif cls in ("mixed_order_R", "mixed_order_AR"):
+            a = int(rng.integers(1, 2 ** 62)) * int(rng.integers(1, 2 ** 62)) % L or 1
+            A = forger.scalarmult_base(a.to_bytes(32, "little"))
+            if cls == "mixed_order_AR":
+                A = forger.point_add(A, ORDER8)
+            r = int(rng.integers(1, 2 ** 62)) * 7919 % L or 1
+            R = forger.point_add(forger.scalarmult_base(r.to_bytes(32, "little")), t8[j % 7])
+            msg = blob[o0 + 64:o1].tobytes()
+            k = int.from_bytes(hashlib.sha512(R + A + msg).digest(), "little") % L
+            sig[:] = np.frombuffer(R + ((r + k * a) % L).to_bytes(32, "little"), np.uint8)
+            pks[i] = np.frombuffer(A, np.uint8)
     return blob, pks, idx, labels
 
 
