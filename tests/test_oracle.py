@@ -85,7 +85,8 @@ def test_sodium_forger_matches_oracle(oracle, sodium):
 
 def test_config3_batch_with_sodium_forger(oracle):
     """configs[2] as bench.py builds it (libsodium forger), small: untouched records valid, mutated
-    ones rejected except mixed-order keys whose k happens to be a multiple of 8."""
+    ones rejected except mixed-order keys whose k happens to be a multiple of 8 and mixed-order
+    (A, R) pairs whose torsion parts cancel."""
     import numpy as np
     import nym_workload
     from adversarial_batch import inject
@@ -97,6 +98,6 @@ def test_config3_batch_with_sodium_forger(oracle):
     mask[idx] = False
     assert got[mask].all()
     lab = np.array(labels)
-    assert not got[idx[lab != "mixed_order_A"]].any()
+    assert not got[idx[(lab != "mixed_order_A") & (lab != "mixed_order_AR")]].any()
     o = np.array([oracle.sign_open_ok(blob2[off[i]:off[i + 1]].tobytes(), pks2[i].tobytes()) for i in idx])
     assert np.array_equal(o, got[idx])
