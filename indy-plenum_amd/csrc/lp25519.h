@@ -28,6 +28,7 @@
 #include "fe25519.h"
 #include "ge25519.h"
 #include "comb.h"
+#include "sc25519.h"
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #define LP_DEVICE 1
@@ -79,6 +80,13 @@ LP_FN void lp_swap32(lu& a, lu& b) {
 }
 LP_FN uint32_t lp_readlane(lu x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
 LP_FN lu lp_gather(const uint32_t* base, lu idx) { return base[idx]; }
+LP_FN uint64_t lp_ballot(lm c) { return __ballot(c); }
+LP_FN lm lp_ne(lu a, uint32_t b) { return a != b; }
+LP_FN lm lp_ltv(lu a, lu b) { return a < b; }
+LP_FN lm lp_or(lm a, lm b) { return a || b; }
+LP_FN lu64 lp_sext64(lu x) { return (uint64_t)(int64_t)(int32_t)x; }
+LP_FN lu64 lp_neg64(lu64 x) { return ~x + 1u; }
+LP_FN lu lp_sar31(lu x) { return (uint32_t)((int32_t)x >> 31); }
 #define LP_CHECK(cond, msg) do { } while (0)
 
 #else  // ---------------------------------------------------------- host simulation (64 lanes)
@@ -152,6 +160,17 @@ LP_FN void lp_swap32(lu& a, lu& b) {
 }
 LP_FN uint32_t lp_readlane(const lu& x, int l) { return x.v[l]; }
 LP_FN lu lp_gather(const uint32_t* base, const lu& idx) { LP_MAP(lu, base[idx.v[l]]); }
+LP_FN uint64_t lp_ballot(const lm& c) {
+    uint64_t m = 0;
+    for (int l = 0; l < 64; l++) m |= (uint64_t)c.v[l] << l;
+    return m;
+}
+LP_FN lm lp_ne(const lu& a, uint32_t b) { LP_MAP(lm, a.v[l] != b); }
+LP_FN lm lp_ltv(const lu& a, const lu& b) { LP_MAP(lm, a.v[l] < b.v[l]); }
+LP_FN lm lp_or(const lm& a, const lm& b) { LP_MAP(lm, a.v[l] || b.v[l]); }
+LP_FN lu64 lp_sext64(const lu& x) { LP_MAP(lu64, (uint64_t)(int64_t)(int32_t)x.v[l]); }
+LP_FN lu64 lp_neg64(const lu64& x) { LP_MAP(lu64, ~x.v[l] + 1u); }
+LP_FN lu lp_sar31(const lu& x) { LP_MAP(lu, (uint32_t)((int32_t)x.v[l] >> 31)); }
 #undef LP_MAP
 #ifdef PV_BOUNDS_CHECK
 #define LP_CHECK(cond, msg) do { if (!(cond)) { fprintf(stderr, "lp bound violated: %s\n", msg); abort(); } } while (0)
@@ -636,4 +655,166 @@ LP_FN bool lp_final_check(const LpLane& c, const LpConsts& K, const lu& QA, cons
     const lu prod = lp_mul(c, c.rows(xr[1], yr[1], 0u, 0u), QZ);
     const lu diff = lp_sub(c, c.rows(QX, QY, 0u, 0u), prod);
     return lp_row_iszero(diff, 0) && lp_row_iszero(diff, 1);
+}
+
+// ------------------------------------------------------------------ the half-size split, limb-parallel
+// sc25519.h sc_halfsize for ONE wave whose lanes all hold the same k (the latency path): the same
+// Lehmer blocks and exact steps, with the multiword state spread over the lanes -- lane 16 r + i holds
+// word i of row r: r0, r1 (9 words, two's complement) and t0, t1 (8 words, mod 2^256) -- so a block's
+// matrix update is two products per lane and a carry pass across the row (DPP row_shr) instead of
+// ~600 dependent scalar instructions. The leading digits and every test are read back with readlane /
+// ballot (uniform control). Same quotients, invariant and fallback as sc_halfsize, so the same split.
+
+// Words of the signed sum P_i 2^(32 i) of per-lane 64-bit partials, per row modulo 2^(32 n) (r rows:
+// n = 9, t rows: n = 8; lanes past the row's words stay 0).
+LP_FN lu lp_mp_norm(const LpLane& c, const lu64& P) {
+    const lm keep = lp_ltv(c.k, lp_sel(lp_lt(c.row, 2u), 9u, 8u));
+    lu64 s = lp_wide(lp_lo(P)) + lp_sext64(lp_shr<1>(lp_hi(P)));
+    lu w = lp_sel(keep, lp_lo(s), 0u);
+    lu cr = lp_sel(keep, lp_hi(s), 0u);
+    for (int it = 0; it < 10; it++) {  // carries of -1 / 0 / +1 ripple one word per pass
+        const lu cin = lp_shr<1>(cr);
+        if (lp_ballot(lp_ne(cin, 0u)) == 0) break;
+        s = lp_wide(w) + lp_sext64(cin);
+        w = lp_sel(keep, lp_lo(s), 0u);
+        cr = lp_sel(keep, lp_hi(s), 0u);
+    }
+    return w;
+}
+// (r0, r1, t0, t1) <- (A r0 + B r1, C r0 + D r1, A t0 + B t1, C t0 + D t1), |A|, |B|, |C|, |D| < 2^31
+LP_FN lu lp_mat_update(const LpLane& c, const lu& st, int64_t A, int64_t B, int64_t C, int64_t D) {
+    lu a = st, b = st;
+    lp_swap16(a, b);  // a = [r0 r0 t0 t0], b = [r1 r1 t1 t1]
+    const lm odd = lp_eq(c.row & 1u, 1u);
+    const int64_t cs[4] = {A, B, C, D};
+    const uint32_t ma[2] = {(uint32_t)(A < 0 ? -A : A), (uint32_t)(C < 0 ? -C : C)};
+    const uint32_t mb[2] = {(uint32_t)(B < 0 ? -B : B), (uint32_t)(D < 0 ? -D : D)};
+    const lu64 pa = lp_mad(a, lp_sel(odd, ma[1], ma[0]), lu64(0u));
+    const lu64 pb = lp_mad(b, lp_sel(odd, mb[1], mb[0]), lu64(0u));
+    const lm na = lp_eq(lp_sel(odd, cs[2] < 0 ? 1u : 0u, cs[0] < 0 ? 1u : 0u), 1u);
+    const lm nb = lp_eq(lp_sel(odd, cs[3] < 0 ? 1u : 0u, cs[1] < 0 ? 1u : 0u), 1u);
+    return lp_mp_norm(c, lp_sel64(na, lp_neg64(pa), pa) + lp_sel64(nb, lp_neg64(pb), pb));
+}
+// 0 <= r1 < r0 (both rows read as 9-word two's complement)
+LP_FN bool lp_pair_ordered(const LpLane& c, const lu& st) {
+    if ((int32_t)lp_readlane(st, 8) < 0 || (int32_t)lp_readlane(st, 24) < 0) return false;
+    lu a = st, b = st;
+    lp_swap16(a, b);
+    const uint64_t gt = lp_ballot(lp_and(lp_eq(c.row, 1u), lp_ltv(a, b)));  // r1 word > r0 word
+    const uint64_t lt = lp_ballot(lp_and(lp_eq(c.row, 1u), lp_ltv(b, a)));
+    if (lt == 0) return false;
+    return gt == 0 || (63 - __builtin_clzll(lt)) > (63 - __builtin_clzll(gt));
+}
+// |t0|, |t1| < 2^168: bits 168..255 of each t row equal its sign
+LP_FN bool lp_t_small(const LpLane& c, const lu& st) {
+    const lu sg = lp_sar31(lp_bcast<7>(st));
+    const lm hi67 = lp_and(lp_ge(c.k, 6u), lp_le(c.k, 7u));
+    const lm bad = lp_and(lp_ge(c.row, 2u),
+                          lp_or(lp_and(hi67, lp_ne(st ^ sg, 0u)), lp_and(lp_eq(c.k, 5u), lp_ne((st ^ sg) >> 8, 0u))));
+    return lp_ballot(bad) == 0;
+}
+
+LP_FN void lp_halfsize(const LpLane& c, pv_halfk& h, const uint32_t k[8]) {
+    lu st = 0u;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        st = lp_sel(lp_eq(lp_lane(), (uint32_t)i), i < 8 ? SC_8L[i] : 0u, st);
+        st = lp_sel(lp_eq(lp_lane(), (uint32_t)(16 + i)), i < 8 ? k[i] : 0u, st);
+    }
+    st = lp_sel(lp_eq(lp_lane(), 48u), 1u, st);  // t1 = 1
+    bool bad = false;
+    // ---- Lehmer blocks while r1 >= 2^131
+    for (int blk = 0; blk < PV_HALF_BLOCKS && !bad; blk++) {
+        const uint64_t nz = lp_ballot(lp_ne(st, 0u));
+        const uint32_t r1nz = (uint32_t)(nz >> 16) & 0x1FFu;
+        if ((r1nz >> 5) == 0 && (lp_readlane(st, 20) >> 3) == 0) break;
+        const int w = 31 - __builtin_clz((uint32_t)nz & 0x1FFu);  // >= 4 (r0 > r1 >= 2^131)
+        const uint32_t a1 = lp_readlane(st, w), a0 = lp_readlane(st, w - 1);
+        const uint32_t b1 = lp_readlane(st, 16 + w), b0 = lp_readlane(st, 15 + w);
+        const int sh = 33 - (int)__builtin_clz(a1);
+        const int s = sh > 0 ? sh : 0;
+        int32_t xh = (int32_t)((((uint64_t)a1 << 32) | a0) >> s);
+        int32_t yh = (int32_t)((((uint64_t)b1 << 32) | b0) >> s);
+        const int e = 32 * (w - 1) + s;
+        const int32_t ythr = e >= 130 ? 1 : (int32_t)(1u << (130 - e));
+        int32_t A = 1, B = 0, C = 0, D = 1;
+        for (int it = 0; it < 24; it++) {
+            const int32_t n1 = xh + A, d1 = yh + C, n2 = xh + B, d2 = yh + D;
+            bool ok1, ok2;
+            const uint32_t q = pv_qdiv31(n1, d1, ok1);
+            const uint32_t q2 = pv_qdiv31(n2, d2, ok2);
+            if (!ok1 || !ok2 || q != q2) break;
+            const int64_t ny = (int64_t)xh - (int64_t)q * yh;
+            const int64_t nC = (int64_t)A - (int64_t)q * C, nD = (int64_t)B - (int64_t)q * D;
+            if (ny < ythr || nC >= 32768 || nC <= -32768 || nD >= 32768 || nD <= -32768) break;
+            A = C;
+            C = (int32_t)nC;
+            B = D;
+            D = (int32_t)nD;
+            xh = yh;
+            yh = (int32_t)ny;
+        }
+        if (B == 0) {
+            // one exact step: q from the top three words, then fixed by whole additions of r0
+            const uint32_t a2 = lp_readlane(st, w - 2), b2 = lp_readlane(st, 14 + w);
+            const double qd = ((double)a1 * 4294967296.0 + (double)a0 + (double)a2 / 4294967296.0) /
+                              ((double)b1 * 4294967296.0 + (double)b0 + (double)b2 / 4294967296.0);
+            if (!(qd < 2147483647.0)) {
+                bad = true;
+                break;
+            }
+            const int64_t q = (int64_t)qd;
+            st = lp_mat_update(c, st, 0, 1, 1, -q);
+            if ((int32_t)lp_readlane(st, 24) < 0) st = lp_mat_update(c, st, 1, 0, 1, 1);
+            else if (!lp_pair_ordered(c, st)) st = lp_mat_update(c, st, 1, 0, -1, 1);
+        } else {
+            st = lp_mat_update(c, st, A, B, C, D);
+        }
+        bad |= !lp_pair_ordered(c, st) || !lp_t_small(c, st);
+    }
+    // ---- exact single steps until r1 < 2^128 with t1 odd
+    for (int it = 0; it < PV_HALF_MAXIT && !bad; it++) {
+        const uint64_t nz = lp_ballot(lp_ne(st, 0u));
+        if ((((uint32_t)(nz >> 16) & 0x1FFu) >> 4) == 0 && (lp_readlane(st, 48) & 1u)) break;
+        const int w = 31 - __builtin_clz(((uint32_t)nz & 0x1FFu) | 1u);
+        if (w < 2 || ((nz >> 16) & 0x1FFu) == 0) {
+            bad = true;
+            break;
+        }
+        const uint32_t a1 = lp_readlane(st, w), a0 = lp_readlane(st, w - 1), a2 = lp_readlane(st, w - 2);
+        const uint32_t b1 = lp_readlane(st, 16 + w), b0 = lp_readlane(st, 15 + w), b2 = lp_readlane(st, 14 + w);
+        const double qd = ((double)a1 * 4294967296.0 + (double)a0 + (double)a2 / 4294967296.0) /
+                          ((double)b1 * 4294967296.0 + (double)b0 + (double)b2 / 4294967296.0);
+        if (!(qd < 2147483647.0)) {
+            bad = true;
+            break;
+        }
+        const int64_t q = (int64_t)qd;
+        st = lp_mat_update(c, st, 0, 1, 1, -q);
+        if ((int32_t)lp_readlane(st, 24) < 0) st = lp_mat_update(c, st, 1, 0, 1, 1);
+        else if (!lp_pair_ordered(c, st)) st = lp_mat_update(c, st, 1, 0, -1, 1);
+        bad |= !lp_pair_ordered(c, st) || !lp_t_small(c, st);
+    }
+    const uint64_t nz = lp_ballot(lp_ne(st, 0u));
+    const bool done = !bad && (((uint32_t)(nz >> 16) & 0x1FFu) >> 4) == 0 && (lp_readlane(st, 48) & 1u);
+    // k2 = |t1|, k1 = r1 with t1's sign moved onto it
+    uint32_t t1[8], ta[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) t1[i] = lp_readlane(st, 48 + i);
+    const bool tneg = (int32_t)t1[7] < 0;
+    uint64_t cy = tneg ? 1u : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t t = (uint64_t)(tneg ? ~t1[i] : t1[i]) + cy;
+        ta[i] = (uint32_t)t;
+        cy = t >> 32;
+    }
+    const bool ok = done && (ta[5] | ta[6] | ta[7]) == 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        h.k1[i] = ok ? lp_readlane(st, 16 + i) : k[i];
+        h.k2[i] = ok ? ta[i] : (i == 0 ? 1u : 0u);
+    }
+    h.neg = ok && tneg;
+    h.fallback = !ok;
 }

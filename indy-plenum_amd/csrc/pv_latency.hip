@@ -148,13 +148,7 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
             S[q] = __builtin_amdgcn_readfirstlane(in.S[q]);
         }
         pv_halfk hk;
-#ifdef PV_LAT_TRACE
-        uint32_t st[3] = {0, 0, 0};
-        sc_halfsize(hk, k, st);
-        if (blockIdx.x == 0 && lane == 0) pv_lat_trace_buf[15] = st[0] | (st[1] << 8) | ((uint64_t)st[2] << 16);
-#else
-        sc_halfsize(hk, k);
-#endif
+        lp_halfsize(c, hk, k);
         LAT_STAMP(12);
         uint32_t s2[8], fs[8], e1[8], e2[8];
         sc_mul(s2, hk.k2, S);
@@ -347,7 +341,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
             S[q] = __builtin_amdgcn_readfirstlane(in.S[q]);
         }
         pv_halfk hk;
-        sc_halfsize(hk, k);
+        lp_halfsize(c, hk, k);
         LAT_STAMP(12);
         uint32_t s2[8], fs[8], e1[8], e2[8];
         sc_mul(s2, hk.k2, S);

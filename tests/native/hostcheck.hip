@@ -310,6 +310,20 @@ int hc_sc_nwin16(const uint8_t* a) {
     return sc_nwin16(e);
 }
 
+// lp_halfsize (the latency path's limb-parallel split) on a 32-byte scalar, same outputs as
+// hc_sc_halfsize
+int hc_lp_halfsize(const uint8_t* k, uint8_t* k1, uint8_t* k2, int* neg) {
+    uint32_t kw[8];
+    load_words(kw, k);
+    const LpLane c = LpLane::make();
+    pv_halfk h;
+    lp_halfsize(c, h, kw);
+    memcpy(k1, h.k1, 32);
+    memcpy(k2, h.k2, 32);
+    *neg = h.neg;
+    return h.fallback;
+}
+
 // The half-size Straus path as the device runs it: pv_prepare_half (checks, +-A, -R', split of k,
 // k2 S mod L), the [j]PA and [j](-R') tables, [k2 S]B from pv_comb_b_acc_w<16> over the radix-65536
 // host table, pv_straus_ar_xyz, encoding compared with R. force_fallback: use (k, 1) as the split (the
@@ -485,7 +499,7 @@ int hc_lp_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     uint32_t k[8];
     pv_hash_k(k, in, smlen, mw);
     pv_halfk hk;
-    sc_halfsize(hk, k);
+    lp_halfsize(c, hk, k);
     uint32_t s2[8], fs[8], e1[8], e2[8];
     sc_mul(s2, hk.k2, in.S);
     sc_recode65536(fs, s2);
@@ -535,7 +549,7 @@ int hc_lp4_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk, int s
     uint32_t k[8];
     pv_hash_k(k, in, smlen, mw);
     pv_halfk hk;
-    sc_halfsize(hk, k);
+    lp_halfsize(c, hk, k);
     uint32_t s2[8], fs[8], e1[8], e2[8];
     sc_mul(s2, hk.k2, in.S);
     sc_recode65536(fs, s2);

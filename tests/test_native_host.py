@@ -390,3 +390,20 @@ def test_straus_half_vs_libsodium(hc, sodium, oracle):
             want = sodium.sign_open_ok(sm, pk)
             got = hc.hc_sign_open_straus_half16(sm, ctypes.c_uint64(len(sm)), pk, 0, i % 2)
             assert bool(got) == want, cls
+
+
+def test_lp_halfsize_matches_per_lane_split(hc):
+    """lp_halfsize (the latency path's limb-parallel split: the multiword state across the lanes of
+    a wave, matrix updates as lane products + DPP carry passes) gives exactly sc_halfsize's split."""
+    rng = random.Random(45)
+    edges = [0, 1, 2 ** 64, 2 ** 128 - 1, 2 ** 128, 2 ** 131 + 5, L - 1, N8L // 3, N8L // 2 ** 33, 2 ** 252]
+    for k in edges + [rng.randrange(L) for _ in range(3000)] + [rng.getrandbits(253) for _ in range(200)]:
+        b = k.to_bytes(32, "little")
+        outs = []
+        for fn in (hc.hc_sc_halfsize, hc.hc_lp_halfsize):
+            k1 = ctypes.create_string_buffer(32)
+            k2 = ctypes.create_string_buffer(32)
+            neg = ctypes.c_int()
+            fb = fn(b, k1, k2, ctypes.byref(neg))
+            outs.append((k1.raw, k2.raw, neg.value, fb))
+        assert outs[0] == outs[1], k
