@@ -1,8 +1,8 @@
 // SHA-512 (FIPS 180-4) for the per-request hash k = SHA-512(R || A || M) of the verify kernels.
 //
 // 64-bit words live in VGPR pairs: additions are single v_lshl_add_u64, every rotation is two
-// v_alignbit_b32 (a funnel shift of the two halves), Ch / Maj / the three-way XORs map to
-// v_bfi_b32 / v_xor_b32, byte swaps to v_perm_b32. Rounds are unrolled 16 at a time with the
+// v_alignbit_b32 (a funnel shift of the two halves), Ch / Maj / the three-way XORs are one
+// v_bitop3_b32 per half, byte swaps to v_perm_b32. Rounds are unrolled 16 at a time with the
 // message schedule in a static 16-word ring and the working variables rotated by renaming, so no
 // register moves or indexed register accesses remain (~34 VALU instructions per round).
 // Replaces libsodium's crypto_hash_sha512 inside crypto_sign_open (reached from the reference via
@@ -43,6 +43,31 @@ PV_HD uint32_t pv_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
 
 PV_HD uint64_t pv_pack64(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
 
+// gfx950 v_bitop3_b32: any bitwise function of three operands in one instruction (truth table
+// over src0 = 0xF0, src1 = 0xCC, src2 = 0xAA): XOR3 = 0x96, Ch = 0xCA, Maj = 0xE8. The compiler
+// does not form it from xor/and/or trees itself (round 2: 292 v_xor_b32 per 16 unrolled rounds).
+template <int TT>
+PV_HD uint32_t pv_bitop3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+#else
+    uint32_t r = 0;
+    for (int i = 0; i < 8; i++)
+        if ((TT >> i) & 1) r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+    return r;
+#endif
+}
+// the halves are joined by a bit cast of a 2-vector, not (hi << 32) | lo: LLVM turns an OR of
+// disjoint halves feeding an addition into two 64-bit additions (+1 v_lshl_add_u64 and a v_mov per use)
+template <int TT>
+PV_HD uint64_t pv_bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 v;
+    v.x = pv_bitop3<TT>((uint32_t)a, (uint32_t)b, (uint32_t)c);
+    v.y = pv_bitop3<TT>((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32));
+    return __builtin_bit_cast(uint64_t, v);
+}
+
 // rotate right by a compile-time n (0 < n < 64, n != 32)
 template <int N>
 PV_HD uint64_t pv_rotr64(uint64_t x) {
@@ -78,11 +103,11 @@ PV_HD void sha512_init(uint64_t st[8]) {
 // One round: the eight working variables rotate by renaming (the caller passes them shifted).
 #define PV_SHA_ROUND(a, b, c, d, e, f, g, h, kw)                                                   \
     do {                                                                                          \
-        const uint64_t S1 = pv_rotr64<14>(e) ^ pv_rotr64<18>(e) ^ pv_rotr64<41>(e);               \
-        const uint64_t ch = g ^ (e & (f ^ g));                                                    \
+        const uint64_t S1 = pv_bitop3_64<0x96>(pv_rotr64<14>(e), pv_rotr64<18>(e), pv_rotr64<41>(e)); \
+        const uint64_t ch = pv_bitop3_64<0xCA>(e, f, g);                                          \
         const uint64_t t1 = h + S1 + ch + (kw);                                                   \
-        const uint64_t S0 = pv_rotr64<28>(a) ^ pv_rotr64<34>(a) ^ pv_rotr64<39>(a);               \
-        const uint64_t mj = (a & b) | (c & (a | b));                                              \
+        const uint64_t S0 = pv_bitop3_64<0x96>(pv_rotr64<28>(a), pv_rotr64<34>(a), pv_rotr64<39>(a)); \
+        const uint64_t mj = pv_bitop3_64<0xE8>(a, b, c);                                          \
         d += t1;                                                                                  \
         h = t1 + S0 + mj;                                                                         \
     } while (0)
@@ -100,8 +125,8 @@ PV_HD void sha512_compress(uint64_t st[8], const uint64_t blk[16]) {
             const int i = r + j;
             if (r > 0) {
                 const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-                const uint64_t s0 = pv_rotr64<1>(w15) ^ pv_rotr64<8>(w15) ^ pv_shr64<7>(w15);
-                const uint64_t s1 = pv_rotr64<19>(w2) ^ pv_rotr64<61>(w2) ^ pv_shr64<6>(w2);
+                const uint64_t s0 = pv_bitop3_64<0x96>(pv_rotr64<1>(w15), pv_rotr64<8>(w15), pv_shr64<7>(w15));
+                const uint64_t s1 = pv_bitop3_64<0x96>(pv_rotr64<19>(w2), pv_rotr64<61>(w2), pv_shr64<6>(w2));
                 w[i & 15] += s0 + w[(i - 7) & 15] + s1;
             }
             const uint64_t kw = PV_K512[i] + w[i & 15];
