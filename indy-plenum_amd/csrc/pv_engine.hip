@@ -44,6 +44,12 @@ static constexpr int PV_BLOCK = 256;
 #ifndef PV_FILL_MINBLOCKS
 #define PV_FILL_MINBLOCKS 2
 #endif
+#ifndef PV_ATAB_NT  // per-request Straus tables read with the streaming (evict-first) cache policy
+#define PV_ATAB_NT 0
+#endif
+#ifndef PV_SIDE_PRIO
+#define PV_SIDE_PRIO 0
+#endif
 #ifndef PV_MSM_MINBLOCKS
 // workgroups per CU the msm kernel's register budget is sized for (3: <= 168 VGPRs, 3 waves/SIMD; the
 // full-length loop fits that at 2 as well)
@@ -203,7 +209,13 @@ struct DevATab {
     __device__ __forceinline__ void load_half(int j, int h, uint32_t w[20]) const {
 #pragma unroll
         for (int q = 0; q < 5; q++) {
+#if PV_ATAB_NT
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(&at(j, 5 * h + q)));
+            const uint4 v = make_uint4(t.x, t.y, t.z, t.w);
+#else
             const uint4 v = at(j, 5 * h + q);
+#endif
             w[4 * q] = v.x;
             w[4 * q + 1] = v.y;
             w[4 * q + 2] = v.z;
@@ -824,21 +836,33 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_seed_kernel(const uint8_t* __
     }
 }
 
-// Dedup 2/2: the owner request of each occupied slot takes a dense key id (one atomic per wave)
-// and records its key's request count.
-__global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, KeyWork kw) {
-    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
+// Dedup 2/2: the owner request of each occupied slot takes a dense key id and records its key's
+// request count. One id atomic per 1,024-thread workgroup (wave counts summed in LDS): the atomics
+// of one address serialise (~8 ns each), and with one per wave a chunk of 7k distinct keys spent
+// ~50 us in them (config 3; 1k keys ~11 us).
+static constexpr int PV_ASSIGN_BLOCK = 1024;
+__global__ __launch_bounds__(PV_ASSIGN_BLOCK) void pv_key_assign_kernel(uint64_t n, KeyWork kw) {
+    __shared__ uint32_t wcnt[PV_ASSIGN_BLOCK / 64 + 1];
+    const uint32_t i = blockIdx.x * PV_ASSIGN_BLOCK + threadIdx.x;
     const uint32_t s = i < n ? kw.req_key[i] : 0u;
     const bool own = i < n && kw.slot[s] == i;
     const uint64_t owners = __ballot(own);
-    if (owners == 0) return;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)owners) - 1u;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&kw.nkeys[PV_SPLIT_KEYS], (uint32_t)__popcll(owners));
-    base = __shfl(base, (int)leader);
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    if (lane == 0) wcnt[wv] = (uint32_t)__popcll(owners);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < PV_ASSIGN_BLOCK / 64; w++) {
+            const uint32_t c = wcnt[w];
+            wcnt[w] = tot;
+            tot += c;
+        }
+        wcnt[PV_ASSIGN_BLOCK / 64] = tot ? atomicAdd(&kw.nkeys[PV_SPLIT_KEYS], tot) : 0u;
+    }
+    __syncthreads();
     if (!own) return;
-    const uint32_t id = base + (uint32_t)__popcll(owners & ((1ull << lane) - 1ull));  // < n
+    const uint32_t id = wcnt[PV_ASSIGN_BLOCK / 64] + wcnt[wv] +
+                        (uint32_t)__popcll(owners & ((1ull << lane) - 1ull));  // < n
     kw.slot_id[s] = id;
     kw.key_owner[id] = i;
     // sub-counts -> offsets (zero counts stay zero: no request reads them); all loads before the stores
@@ -886,6 +910,7 @@ __device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
 // Comb keys (>= min_req requests, the first kcap of them in id order) take slots [0, CS) in id
 // order, every other key's requests the slots [CS, n). Threads own contiguous id ranges; three
 // passes over key_count: comb index, slot totals, cursors.
+static constexpr uint32_t PV_SCAN_REG = 16;  // key counts a scan thread keeps in registers
 __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uint32_t* __restrict__ kc_flags) {
     __shared__ uint32_t part[1024];
     const uint32_t nk = kw.nkeys[PV_SPLIT_KEYS];
@@ -898,13 +923,26 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
     auto is_cand = [&](uint32_t id, uint32_t c) {
         return all_comb || c >= kw.min_req || (kw.kc_on && kw.key_cslot[id] != PV_EMPTY);
     };
+    // up to 16k keys every count is loaded once, all loads in flight together (three dependent
+    // passes of L2 reads took ~18 us at 7k keys); above that the passes re-read
+    const bool reg = per <= PV_SCAN_REG;
+    uint32_t cr[PV_SCAN_REG];
+#pragma unroll
+    for (uint32_t u = 0; u < PV_SCAN_REG; u++) cr[u] = reg && lo + u < hi ? kw.key_count[lo + u] : 0u;
+    auto count = [&](uint32_t id) -> uint32_t {
+        if (!reg) return kw.key_count[id];
+        uint32_t c = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < PV_SCAN_REG; u++) c = id - lo == u ? cr[u] : c;
+        return c;
+    };
     uint32_t cand = 0;
-    for (uint32_t id = lo; id < hi; id++) cand += is_cand(id, kw.key_count[id]) ? 1u : 0u;
+    for (uint32_t id = lo; id < hi; id++) cand += is_cand(id, count(id)) ? 1u : 0u;
     uint32_t ncand;
     const uint32_t jbase = pv_block_scan(cand, part, &ncand);
     uint32_t cs = 0, ss = 0;
     for (uint32_t id = lo, j = jbase; id < hi; id++) {
-        const uint32_t c = kw.key_count[id];
+        const uint32_t c = count(id);
         if (is_cand(id, c) && j++ < kw.kcap) cs += c;
         else ss += c;
     }
@@ -912,7 +950,7 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
     uint32_t cc = pv_block_scan(cs, part, &ctotal);
     uint32_t sc = ctotal + pv_block_scan(ss, part, &stotal);
     for (uint32_t id = lo, j = jbase; id < hi; id++) {
-        const uint32_t c = kw.key_count[id];
+        const uint32_t c = count(id);
         const bool cand_id = is_cand(id, c);
         if (cand_id && j < kw.kcap) {
             const uint32_t cslot = kw.kc_on ? kw.key_cslot[id] : PV_EMPTY;
@@ -1965,7 +2003,8 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             }
             hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
+            hipLaunchKernelGGL(pv_key_assign_kernel, dim3((unsigned)((m + PV_ASSIGN_BLOCK - 1) / PV_ASSIGN_BLOCK)),
+                               dim3(PV_ASSIGN_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             if (kc_active) {
                 hipLaunchKernelGGL(pv_key_cache_probe_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0,
@@ -2140,13 +2179,32 @@ int pv_init(int device) {
         return fail(PV_ERR_NO_DEVICE, std::string("pv_init: built for gfx950, device is ") + prop.gcnArchName);
     g_ctx.cus = prop.multiProcessorCount;
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+#if PV_SIDE_PRIO >= 2
+    {
+        int least = 0, greatest = 0;
+        PV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest), PV_ERR_NO_DEVICE);
+        PV_HIP(hipStreamCreateWithPriority(&g_ctx.kstream, hipStreamNonBlocking, greatest), PV_ERR_NO_DEVICE);
+    }
+#else
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.kstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+#endif
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_keys_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.fstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     for (auto& e : g_ctx.ev_chain) PV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_prep_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+#if PV_SIDE_PRIO
+    {
+        // Straus-side requests (one-off keys) are a short dependent chain of small grids; a
+        // high-priority queue lets their workgroups dispatch ahead of the comb grids so the
+        // chain ends before comb_a instead of overlapping it.
+        int least = 0, greatest = 0;
+        PV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest), PV_ERR_NO_DEVICE);
+        PV_HIP(hipStreamCreateWithPriority(&g_ctx.sstream, hipStreamNonBlocking, greatest), PV_ERR_NO_DEVICE);
+    }
+#else
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+#endif
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_verdict_copied, hipEventDisableTiming), PV_ERR_NO_DEVICE);

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--first-kernel", default="pv_key_insert_kernel")
+    ap.add_argument("--summary", action="store_true",
+                    help="one line per step of the whole trace: span and the main kernels' durations (us)")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     cur = con.execute("select * from kernels limit 1")
@@ -30,6 +32,25 @@ def main():
     starts = [i for i, r in enumerate(rows) if r[0] == a.first_kernel]
     if not starts:
         raise SystemExit("no %s in the trace (columns: %s)" % (a.first_kernel, cols))
+    if a.summary:
+        keys = ("pv_key_assign_kernel", "pv_key_scan_kernel", "pv_key_chain_lp_kernel", "pv_key_fill_kernel",
+                "pv_comb_b_kernel", "pv_comb_a_kernel", "pv_msm_kernel", "pv_encode_kernel")
+        print("row    span   " + " ".join("%8s" % k.replace("pv_", "").replace("_kernel", "")[:8] for k in keys)
+              + "  comb_a_start")
+        for j, s in enumerate(starts):
+            nxt = starts[j + 1] if j + 1 < len(starts) else len(rows)
+            t0 = rows[s][1]
+            span = (max(r[2] for r in rows[s:nxt]) - t0) / 1e3
+            dur = {}
+            ca = 0.0
+            for name, st, en, _ in rows[s:nxt]:
+                for k in keys:
+                    if name.endswith(k) or name.startswith("void " + k):
+                        dur[k] = dur.get(k, 0.0) + (en - st) / 1e3
+                if "pv_comb_a_kernel" in name:
+                    ca = (st - t0) / 1e3
+            print("%5d %7.1f " % (s, span) + " ".join("%8.1f" % dur.get(k, 0.0) for k in keys) + "  %8.1f" % ca)
+        return
     for s in starts[-a.steps:]:
         t0 = rows[s][1]
         nxt = next((i for i in starts if i > s), len(rows))

@@ -1,10 +1,11 @@
 #!/bin/bash
 # Kernel timeline of the bench's configs[2] leg (2 % adversarial, AUTO split into comb keys and a
 # Straus side stream) and of the headline for comparison. Run on the GPU box from the repo root:
-#   tools/trace_config3.sh  -> gpurun_out/c3trace/{timeline_headline,timeline_config3}.txt
+#   tools/trace_config3.sh [TAG]  -> gpurun_out/c3trace[_TAG]/{timeline_headline,timeline_config3,steps}.txt
+# (PLENUM_AMD_LIB selects a variant library as everywhere else)
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/c3trace
+OUT=gpurun_out/c3trace${1:+_$1}
 mkdir -p $OUT
 DS=/tmp/nym_c3.npz
 timeout -k 10 300 python3 tools/nym_workload.py --out $DS > /dev/null || exit $?
@@ -15,4 +16,5 @@ echo "db: $DB"
 # the config3 leg runs after the headline: its steps are the last ones in the trace
 python3 tools/timeline.py "$DB" --steps 2 > $OUT/timeline_config3.txt || exit $?
 python3 tools/timeline.py "$DB" --steps 9 | head -60 > $OUT/timeline_headline.txt || true
-cat $OUT/timeline_config3.txt
+python3 tools/timeline.py "$DB" --summary > $OUT/steps.txt || exit $?
+cat $OUT/steps.txt
