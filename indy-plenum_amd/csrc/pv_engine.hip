@@ -44,6 +44,12 @@ static constexpr int PV_BLOCK = 256;
 #ifndef PV_FILL_MINBLOCKS
 #define PV_FILL_MINBLOCKS 2
 #endif
+// [S]B of a keyed chunk per request from the chunk's start, beside the dedup (A/B knob, off): the
+// dedup's atomics slow 2-4x under it and the headline gains nothing measurable; config 3 loses
+// 0.1 ms (profiles/r03/half/ab_comb_b_early)
+#ifndef PV_COMB_B_EARLY
+#define PV_COMB_B_EARLY 0
+#endif
 #ifndef PV_ATAB_NT  // per-request Straus tables read with the streaming (evict-first) cache policy
 #define PV_ATAB_NT 0
 #endif
@@ -316,6 +322,7 @@ struct Work {
     uint32_t* digits;
     uint32_t* flags;
     uint32_t* q;
+    uint4* qb;        // [S]B per REQUEST of a keyed chunk, 160 B each (pv_comb_b_req_kernel)
     uint64_t stride;  // chunk capacity (requests)
 };
 
@@ -840,7 +847,9 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_seed_kernel(const uint8_t* __
 // request count. One id atomic per 1,024-thread workgroup (wave counts summed in LDS): the atomics
 // of one address serialise (~8 ns each), and with one per wave a chunk of 7k distinct keys spent
 // ~50 us in them (config 3; 1k keys ~11 us).
-static constexpr int PV_ASSIGN_BLOCK = 1024;
+#ifndef PV_ASSIGN_BLOCK
+#define PV_ASSIGN_BLOCK 1024
+#endif
 __global__ __launch_bounds__(PV_ASSIGN_BLOCK) void pv_key_assign_kernel(uint64_t n, KeyWork kw) {
     __shared__ uint32_t wcnt[PV_ASSIGN_BLOCK / 64 + 1];
     const uint32_t i = blockIdx.x * PV_ASSIGN_BLOCK + threadIdx.x;
@@ -1510,6 +1519,50 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
     }
 }
 
+// Keyed chunk, [S]B per REQUEST (not slot): needs only S, so it starts with the chunk on its own
+// stream and runs beside the dedup kernels (atomics and scattered stores that leave the ALUs idle for
+// ~0.14 ms) instead of after the key sort. acc (extended, 40 words) to qb[r], 160 contiguous bytes,
+// which pv_comb_a_kernel gathers by slot_req. Requests of Straus keys get a value nobody reads.
+template <int W>
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_req_kernel(const uint8_t* __restrict__ sm,
+                                                                     const uint64_t* __restrict__ off, uint64_t n,
+                                                                     Work wk, const uint4* __restrict__ bcomb) {
+    const uint32_t r0 = blockIdx.x * PV_BLOCK + threadIdx.x;  // request
+    if (blockIdx.x * PV_BLOCK >= n) return;
+    const uint32_t r = r0 < n ? r0 : (uint32_t)n - 1;  // whole waves stay in step for the staging
+    uint32_t S[8];
+    {
+        const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[r]);
+        const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+#pragma unroll
+        for (int q = 0; q < 8; q++) S[q] = mw.dw(8 + q);
+    }
+    constexpr int P = Bc2<W>::POS;
+    int32_t fb[P];
+    sc_recode_w<W, P>(fb, S);  // any S (an S >= L is rejected by the prep's check)
+    __shared__ uint4 stg[PV_BLOCK / 64][PV_BCOMB_STRIDE / 4][64];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    ge_p3 acc;
+    pv_comb_b_acc_w<P>(acc, DevB2Stage<Bc2<W>::ENT>{bcomb, &stg[wv][0][0], threadIdx.x & 63u}, [&](int j) {
+        int32_t d = 0;
+#pragma unroll
+        for (int u = 0; u < P; u++) d = j == u ? fb[u] : d;
+        return (int)d;
+    });
+    if (r0 >= n) return;
+    uint4* o = wk.qb + (uint64_t)r * 10u;
+    uint32_t w[40];
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        w[q] = acc.X.v[q];
+        w[10 + q] = acc.Y.v[q];
+        w[20 + q] = acc.Z.v[q];
+        w[30 + q] = acc.T.v[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 10; q++) o[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
 // Straus path, [S]B of every Straus slot from the wide fixed-base comb (tiles from the end of the
 // slot range, like the other Straus kernels), extended, to q rows 0..39 for pv_msm_kernel.
 template <int W>
@@ -1610,6 +1663,27 @@ __device__ __forceinline__ void pv_comb_a_slot(const Work& wk, const KeyWork& kw
     const uint32_t S = (uint32_t)wk.stride;
     const Soa qs(wk.q, 40, wk.stride);
     ge_p3 acc;
+#if PV_COMB_B_EARLY
+    {
+        const uint4* a = wk.qb + (uint64_t)kw.slot_req[i] * 10u;  // [S]B of the slot's request
+        uint32_t w[40];
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            const uint4 v = a[q];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            acc.X.v[q] = w[q];
+            acc.Y.v[q] = w[10 + q];
+            acc.Z.v[q] = w[20 + q];
+            acc.T.v[q] = w[30 + q];
+        }
+    }
+#else
 #pragma unroll
     for (int q = 0; q < 10; q++) {
         acc.X.v[q] = qs.ld(q, i);
@@ -1617,6 +1691,7 @@ __device__ __forceinline__ void pv_comb_a_slot(const Work& wk, const KeyWork& kw
         acc.Z.v[q] = qs.ld(20 + q, i);
         acc.T.v[q] = qs.ld(30 + q, i);
     }
+#endif
     const DevDigits dig{wk.digits, S, i};
     fe X, Y, Z;
 #if PV_COMB_PIPELINE
@@ -1726,6 +1801,8 @@ struct Ctx {
     hipStream_t fstream = nullptr;           // table fill, one launch per chain part
     hipEvent_t ev_chain[PV_CHAIN_PARTS] = {};  // chain part done (kstream -> fstream)
     hipEvent_t ev_prep_done = nullptr;        // comb_prep done: need masks ready (main -> fstream)
+    hipStream_t bstream = nullptr;           // [S]B per request of a keyed chunk (PV_COMB_B_EARLY)
+    hipEvent_t ev_b_start = nullptr, ev_b_done = nullptr;
     hipStream_t sstream = nullptr;           // Straus-path slots of a split chunk, overlapped
     hipEvent_t ev_straus_done = nullptr;     // their q / flags written (sstream -> main)
     // Workspace hand-over between callers' streams: every launch ends by recording ev_launch_done
@@ -1994,6 +2071,23 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                        PV_ERR_LAUNCH);
             }
             g_ctx.slots_dirty = true;  // until this chunk's unpermute kernel is enqueued
+#if PV_COMB_B_EARLY
+            // [S]B per request on bstream from the chunk's start (after everything already on the
+            // main stream, e.g. the previous chunk's comb_a reading qb); joined before comb_a
+            auto launch_b_early = [&]() -> int {
+                PV_HIP(hipEventRecord(g_ctx.ev_b_start, stream), PV_ERR_LAUNCH);
+                PV_HIP(hipStreamWaitEvent(g_ctx.bstream, g_ctx.ev_b_start, 0), PV_ERR_LAUNCH);
+                PV_LAUNCH_BC2(pv_comb_b_req_kernel, dim3(grid), dim3(PV_BLOCK), 0, g_ctx.bstream, d_sm, d_off + c0, m,
+                              g_ctx.work, g_ctx.d_bc2);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+                PV_HIP(hipEventRecord(g_ctx.ev_b_done, g_ctx.bstream), PV_ERR_LAUNCH);
+                return PV_OK;
+            };
+#ifndef PV_COMB_B_AFTER
+#define PV_COMB_B_AFTER 0  // 0: at the chunk's start, 1: after the insert kernel
+#endif
+            if (PV_COMB_B_AFTER == 0 && (rc = launch_b_early())) return rc;
+#endif
             // kw.nkeys is cleared by pv_key_insert_kernel (m >= 1 here: the grid has a thread 0)
             if (PV_KEY_SEED > 0 && m > 16ull * PV_KEY_SEED) {  // small chunks: no contention worth a launch
                 const uint64_t ms = std::min<uint64_t>(m, PV_KEY_SEED);
@@ -2003,6 +2097,9 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             }
             hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#if PV_COMB_B_EARLY
+            if (PV_COMB_B_AFTER == 1 && (rc = launch_b_early())) return rc;
+#endif
             hipLaunchKernelGGL(pv_key_assign_kernel, dim3((unsigned)((m + PV_ASSIGN_BLOCK - 1) / PV_ASSIGN_BLOCK)),
                                dim3(PV_ASSIGN_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -2095,10 +2192,14 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
+#if PV_COMB_B_EARLY
+            PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_b_done, 0), PV_ERR_LAUNCH);
+#else
             // [S]B while the key stream finishes the tables, then join
             PV_LAUNCH_BC2(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
                                gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#endif
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
             hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
@@ -2206,6 +2307,9 @@ int pv_init(int device) {
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
 #endif
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipStreamCreateWithFlags(&g_ctx.bstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_start, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_verdict_copied, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     std::vector<uint32_t> bt(PV_BTAB_ENTRIES * PV_BTAB_STRIDE);
@@ -2218,6 +2322,7 @@ int pv_init(int device) {
     PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * PV_DIGIT_ROWS * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 40 * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&g_ctx.work.qb, S * 160), PV_ERR_ALLOC);
     {
         KeyWork& kw = g_ctx.kw;
         const uint64_t H = 2 * S;
@@ -2326,6 +2431,7 @@ void pv_shutdown(void) {
     if (g_ctx.work.digits) (void)hipFree(g_ctx.work.digits);
     if (g_ctx.work.flags) (void)hipFree(g_ctx.work.flags);
     if (g_ctx.work.q) (void)hipFree(g_ctx.work.q);
+    if (g_ctx.work.qb) (void)hipFree(g_ctx.work.qb);
     for (void* p : {(void*)g_ctx.kw.slot, (void*)g_ctx.kw.slot_id, (void*)g_ctx.kw.slot_cnt, (void*)g_ctx.kw.req_key,
                     (void*)g_ctx.kw.req_rank, (void*)g_ctx.kw.nkeys,
                     (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_cid, (void*)g_ctx.kw.comb_key,
@@ -2346,6 +2452,9 @@ void pv_shutdown(void) {
         if (e) (void)hipEventDestroy(e);
     if (g_ctx.ev_prep_done) (void)hipEventDestroy(g_ctx.ev_prep_done);
     if (g_ctx.sstream) (void)hipStreamDestroy(g_ctx.sstream);
+    if (g_ctx.bstream) (void)hipStreamDestroy(g_ctx.bstream);
+    if (g_ctx.ev_b_start) (void)hipEventDestroy(g_ctx.ev_b_start);
+    if (g_ctx.ev_b_done) (void)hipEventDestroy(g_ctx.ev_b_done);
     if (g_ctx.ev_straus_done) (void)hipEventDestroy(g_ctx.ev_straus_done);
     if (g_ctx.ev_launch_done) (void)hipEventDestroy(g_ctx.ev_launch_done);
     if (g_ctx.ev_verdict_copied) (void)hipEventDestroy(g_ctx.ev_verdict_copied);
