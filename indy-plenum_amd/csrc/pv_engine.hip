@@ -2322,7 +2322,9 @@ int pv_init(int device) {
     PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * PV_DIGIT_ROWS * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 40 * 4), PV_ERR_ALLOC);
+#if PV_COMB_B_EARLY
     PV_HIP(hipMalloc((void**)&g_ctx.work.qb, S * 160), PV_ERR_ALLOC);
+#endif
     {
         KeyWork& kw = g_ctx.kw;
         const uint64_t H = 2 * S;
