@@ -375,6 +375,21 @@ def pmc_traffic(kernel):
         return None
 
 
+def pmc_valu_issue(kernel, cus=256):
+    """VALU issue rate of `kernel` from the committed PMC summary: wave-instructions (SQ_INSTS_VALU) per
+    CU-cycle over its dispatch under the counters (eff. clock = GRBM_GUI_ACTIVE / dispatch time). A
+    full-rate wave64 VALU instruction holds a 16-lane SIMD for 4 cycles, so 4 SIMDs issue at most
+    ~1 per CU-cycle: a value near 1 means the kernel is bound by instruction issue, not memory."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            k = json.load(f)["kernels"][kernel]
+        c = k["counters_per_dispatch"]
+        return round(c["SQ_INSTS_VALU"] / (k["median_dispatch_s_under_pmc"] * k["eff_clock_GHz"] * 1e9 * cus), 3)
+    except Exception:
+        return None
+
+
 CONFIG5_TOTAL = 1 << 26  # configs[4]: 64M requests over the node's GPUs
 
 
@@ -732,7 +747,8 @@ def main():
                      "unit": "TMAC/s (v_mad_u64_u32 int32 MACs)", "frac": round(achieved / BC.PEAK_MAC_PER_S, 4),
                      "traffic": pmc_traffic("pv_comb_a_kernel" if comb else "pv_msm_kernel"),
                      "algorithmic_mac_per_verify": round(mac_kernel), "launch_ms": round(launch_ms, 4),
-                     "frac_of_measured_mad_stream": round(achieved / BC.MEASURED_MAD_STREAM_MAC_PER_S, 4)},
+                     "frac_of_measured_mad_stream": round(achieved / BC.MEASURED_MAD_STREAM_MAC_PER_S, 4),
+                     "valu_issue_per_cu_cycle_pmc": pmc_valu_issue("pv_comb_a_kernel" if comb else "pv_msm_kernel")},
         "pipeline": {**{s + "_ms": round(v, 4) for s, v in stage_ms.items()},
                      "kernel_verifies_per_s_per_gpu": round(per_gpu_rate, 1),
                      "whole_pipeline_valu_frac": round(mac_executed * per_gpu_rate / BC.PEAK_MAC_PER_S, 4),
@@ -790,7 +806,8 @@ def main():
                          "frac": round(ach2 / BC.PEAK_MAC_PER_S, 4),
                          "algorithmic_mac_per_verify": round(BC.MAC_MSM_HALF_KERNEL),
                          "algorithm": "half-size split k = k1/k2 mod 8L, 32 windows of both scalars",
-                         "traffic": pmc_traffic("pv_msm_kernel")},
+                         "traffic": pmc_traffic("pv_msm_kernel"),
+                         "valu_issue_per_cu_cycle_pmc": pmc_valu_issue("pv_msm_kernel")},
             "verdicts_ok": ok2}
     c3 = None
     if rank == 0 and world == 1 and not args.no_config3:
