@@ -337,6 +337,15 @@ static constexpr int PV_SPLIT_SLOTS = 2;       // requests (slots) of those keys
 static constexpr int PV_SPLIT_SPARSE = 3;      // 1: the comb tables are filled sparsely (small chunk)
 static constexpr int PV_SPLIT_LAT = 4;         // 1: the dedup chose the latency path for this chunk
 static constexpr uint32_t PV_SPLIT_WORDS = 8;  // counters cleared per keyed chunk
+static constexpr uint32_t PV_NSEG = 8;         // key-id segments (pv_key_assign_kernel)
+// segment g's id counter: word PV_SEG_BASE + g * PV_SEG_STRIDE of the split buffer, one counter per
+// 1 KB so that the segments' atomics land on different memory channels (same-line counters
+// serialise like one)
+#ifndef PV_SEG_STRIDE
+#define PV_SEG_STRIDE 256
+#endif
+static constexpr uint32_t PV_SEG_BASE = 256;
+static constexpr uint32_t PV_SPLIT_ALLOC_WORDS = PV_SEG_BASE + PV_NSEG * PV_SEG_STRIDE;
 struct Gate {
     const uint32_t* split;
     const uint32_t* slot_req;
@@ -410,6 +419,7 @@ struct KeyWork {
     uint32_t kc_on;    // this launch consults the key cache (pv_key_cache_probe_kernel ran)
     uint32_t chunk_n;  // requests in this chunk
     uint32_t lat_choice;  // the scan picks latency vs keyed for this chunk (AUTO, device-buffer call)
+    uint32_t seg_cap;     // key ids of segment s are s * seg_cap + [0, its counter)
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 #ifndef PV_COMB_MIN_REQ
@@ -795,6 +805,7 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* 
     // the chunk's split counters start at 0 (the assign kernel, next on the stream, counts keys into
     // them); done here instead of a separate hipMemsetAsync (~11 us of dispatch + gap per chunk)
     if (i < PV_SPLIT_WORDS) kw.nkeys[i] = 0u;
+    if (i < PV_NSEG) kw.nkeys[PV_SEG_BASE + i * PV_SEG_STRIDE] = 0u;
     if (i >= n) return;
     uint32_t A[8];
     pv_load_pk(A, pk, i);
@@ -843,35 +854,26 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_seed_kernel(const uint8_t* __
     }
 }
 
-// Dedup 2/2: the owner request of each occupied slot takes a dense key id and records its key's
-// request count. One id atomic per 1,024-thread workgroup (wave counts summed in LDS): the atomics
-// of one address serialise (~8 ns each), and with one per wave a chunk of 7k distinct keys spent
-// ~50 us in them (config 3; 1k keys ~11 us).
-#ifndef PV_ASSIGN_BLOCK
-#define PV_ASSIGN_BLOCK 1024
-#endif
-__global__ __launch_bounds__(PV_ASSIGN_BLOCK) void pv_key_assign_kernel(uint64_t n, KeyWork kw) {
-    __shared__ uint32_t wcnt[PV_ASSIGN_BLOCK / 64 + 1];
-    const uint32_t i = blockIdx.x * PV_ASSIGN_BLOCK + threadIdx.x;
+// Dedup 2/2: the owner request of each occupied slot takes a key id and records its key's request
+// count. One atomic per wave that owns keys, on one of PV_NSEG counters (the wave's index mod
+// PV_NSEG): same-address atomics serialise (~7 ns each), and with one counter a chunk of 7k distinct
+// keys spent ~50 us in them (config 3), against ~11 us at 1,024 keys. Ids are segment-major
+// (s * seg_cap + rank in segment s: a segment holds at most seg_cap requests, so it never
+// overflows); the scan kernel walks the segments in order.
+__global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, KeyWork kw) {
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t s = i < n ? kw.req_key[i] : 0u;
     const bool own = i < n && kw.slot[s] == i;
     const uint64_t owners = __ballot(own);
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    if (lane == 0) wcnt[wv] = (uint32_t)__popcll(owners);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (int w = 0; w < PV_ASSIGN_BLOCK / 64; w++) {
-            const uint32_t c = wcnt[w];
-            wcnt[w] = tot;
-            tot += c;
-        }
-        wcnt[PV_ASSIGN_BLOCK / 64] = tot ? atomicAdd(&kw.nkeys[PV_SPLIT_KEYS], tot) : 0u;
-    }
-    __syncthreads();
+    if (owners == 0) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t seg = (i >> 6) & (PV_NSEG - 1u);
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)owners) - 1u;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&kw.nkeys[PV_SEG_BASE + seg * PV_SEG_STRIDE], (uint32_t)__popcll(owners));
+    base = __shfl(base, (int)leader);
     if (!own) return;
-    const uint32_t id = wcnt[PV_ASSIGN_BLOCK / 64] + wcnt[wv] +
-                        (uint32_t)__popcll(owners & ((1ull << lane) - 1ull));  // < n
+    const uint32_t id = seg * kw.seg_cap + base + (uint32_t)__popcll(owners & ((1ull << lane) - 1ull));
     kw.slot_id[s] = id;
     kw.key_owner[id] = i;
     // sub-counts -> offsets (zero counts stay zero: no request reads them); all loads before the stores
@@ -892,8 +894,9 @@ __global__ __launch_bounds__(PV_ASSIGN_BLOCK) void pv_key_assign_kernel(uint64_t
 // in the cache (keycache.h); key_cslot[id] = its cache slot or PV_EMPTY.
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_cache_probe_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
                                                                        PvKeyCacheView kc) {
-    const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;
-    if (id >= kw.nkeys[PV_SPLIT_KEYS]) return;
+    const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;  // grid: PV_NSEG * seg_cap ids
+    const uint32_t seg = id / kw.seg_cap;
+    if (seg >= PV_NSEG || id - seg * kw.seg_cap >= kw.nkeys[PV_SEG_BASE + seg * PV_SEG_STRIDE]) return;
     uint32_t A[8];
     pv_load_pk(A, pk, kw.key_owner[id]);
     kw.key_cslot[id] = pv_kc_lookup(kc, A);
@@ -922,7 +925,19 @@ __device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
 static constexpr uint32_t PV_SCAN_REG = 16;  // key counts a scan thread keeps in registers
 __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uint32_t* __restrict__ kc_flags) {
     __shared__ uint32_t part[1024];
-    const uint32_t nk = kw.nkeys[PV_SPLIT_KEYS];
+    // the key ids are segment-major (pv_key_assign_kernel): v-th key in segment order = id vid(v)
+    uint32_t pre[PV_NSEG + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < PV_NSEG; g++) pre[g + 1] = pre[g] + kw.nkeys[PV_SEG_BASE + g * PV_SEG_STRIDE];
+    const uint32_t nk = pre[PV_NSEG];
+    auto vid = [&](uint32_t v) -> uint32_t {
+        uint32_t id = v;
+#pragma unroll
+        for (uint32_t g = 1; g < PV_NSEG; g++)
+            if (v >= pre[g]) id = v - pre[g] + g * kw.seg_cap;
+        return id;
+    };
     const uint32_t t = threadIdx.x;
     const uint32_t per = (nk + 1023) / 1024;
     const uint32_t lo = min(t * per, nk), hi = min(lo + per, nk);
@@ -937,29 +952,34 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
     const bool reg = per <= PV_SCAN_REG;
     uint32_t cr[PV_SCAN_REG];
 #pragma unroll
-    for (uint32_t u = 0; u < PV_SCAN_REG; u++) cr[u] = reg && lo + u < hi ? kw.key_count[lo + u] : 0u;
-    auto count = [&](uint32_t id) -> uint32_t {
+    for (uint32_t u = 0; u < PV_SCAN_REG; u++) cr[u] = reg && lo + u < hi ? kw.key_count[vid(lo + u)] : 0u;
+    auto count = [&](uint32_t v, uint32_t id) -> uint32_t {
         if (!reg) return kw.key_count[id];
         uint32_t c = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < PV_SCAN_REG; u++) c = id - lo == u ? cr[u] : c;
+        for (uint32_t u = 0; u < PV_SCAN_REG; u++) c = v - lo == u ? cr[u] : c;
         return c;
     };
     uint32_t cand = 0;
-    for (uint32_t id = lo; id < hi; id++) cand += is_cand(id, count(id)) ? 1u : 0u;
+    for (uint32_t v = lo; v < hi; v++) {
+        const uint32_t id = vid(v);
+        cand += is_cand(id, count(v, id)) ? 1u : 0u;
+    }
     uint32_t ncand;
     const uint32_t jbase = pv_block_scan(cand, part, &ncand);
     uint32_t cs = 0, ss = 0;
-    for (uint32_t id = lo, j = jbase; id < hi; id++) {
-        const uint32_t c = count(id);
+    for (uint32_t v = lo, j = jbase; v < hi; v++) {
+        const uint32_t id = vid(v);
+        const uint32_t c = count(v, id);
         if (is_cand(id, c) && j++ < kw.kcap) cs += c;
         else ss += c;
     }
     uint32_t ctotal, stotal;
     uint32_t cc = pv_block_scan(cs, part, &ctotal);
     uint32_t sc = ctotal + pv_block_scan(ss, part, &stotal);
-    for (uint32_t id = lo, j = jbase; id < hi; id++) {
-        const uint32_t c = count(id);
+    for (uint32_t v = lo, j = jbase; v < hi; v++) {
+        const uint32_t id = vid(v);
+        const uint32_t c = count(v, id);
         const bool cand_id = is_cand(id, c);
         if (cand_id && j < kw.kcap) {
             const uint32_t cslot = kw.kc_on ? kw.key_cslot[id] : PV_EMPTY;
@@ -978,6 +998,7 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
         if (cand_id) j++;
     }
     if (t == 0) {
+        kw.nkeys[PV_SPLIT_KEYS] = nk;  // distinct keys (pv_last_path)
         // AUTO's device-side choice for a 2,049..4,096-request batch of pv_verify_batch_device: the
         // rule pv_keyed_hint applies on the host (>= 3 requests per key, every key a comb key) now
         // that the dedup has counted the keys; otherwise the latency kernel runs after this chunk
@@ -2057,6 +2078,8 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         kw.min_req = g_ctx.path == PV_PATH_COMB ? 1u : (uint32_t)PV_COMB_MIN_REQ;
         kw.kc_on = kc_active ? 1u : 0u;
         kw.chunk_n = (uint32_t)m;
+        // a key-id segment holds the owners among its waves (every PV_NSEG-th wave of the chunk)
+        kw.seg_cap = (uint32_t)((((m + 63) / 64) + PV_NSEG - 1) / PV_NSEG * 64);
         kw.lat_choice = dev_choice ? 1u : 0u;
         kw.kc_tab = g_ctx.kc.d_tab;
         const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
@@ -2100,11 +2123,11 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
 #if PV_COMB_B_EARLY
             if (PV_COMB_B_AFTER == 1 && (rc = launch_b_early())) return rc;
 #endif
-            hipLaunchKernelGGL(pv_key_assign_kernel, dim3((unsigned)((m + PV_ASSIGN_BLOCK - 1) / PV_ASSIGN_BLOCK)),
-                               dim3(PV_ASSIGN_BLOCK), 0, stream, m, kw);
+            hipLaunchKernelGGL(pv_key_assign_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             if (kc_active) {
-                hipLaunchKernelGGL(pv_key_cache_probe_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0,
+                hipLaunchKernelGGL(pv_key_cache_probe_kernel, dim3((PV_NSEG * kw.seg_cap + PV_BLOCK - 1) / PV_BLOCK),
+                                   dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0,
                                    kw, kcv);
                 PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             }
@@ -2336,20 +2359,20 @@ int pv_init(int device) {
         PV_HIP(hipMalloc((void**)&kw.slot_cnt, H * 4 * PV_RANK_SUB), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_key, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_rank, S * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.nkeys, 256), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_owner, S * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_cid, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.nkeys, PV_SPLIT_ALLOC_WORDS * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_owner, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
+        PV_HIP(hipMalloc((void**)&kw.key_cid, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
         PV_HIP(hipMalloc((void**)&kw.comb_key, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_PTS * 160), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_count, S * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_cursor, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_count, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
+        PV_HIP(hipMalloc((void**)&kw.key_cursor, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
         PV_HIP(hipMalloc((void**)&kw.slot_req, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.req_pos, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.skey, S * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.sverdict, S / 64 * 8), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_cslot, S * 4), PV_ERR_ALLOC);
+        PV_HIP(hipMalloc((void**)&kw.key_cslot, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
         PV_HIP(hipMalloc((void**)&kw.comb_cslot, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
         PV_HIP(hipMalloc((void**)&kw.need, (uint64_t)PV_ALLCOMB_KEYS * PV_COMB_POS * 5 * 4), PV_ERR_ALLOC);
         PV_HIP(hipMemset(kw.comb_cslot, 0xFF, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
