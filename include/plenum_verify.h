@@ -64,7 +64,12 @@ void pv_shutdown(void);
 const char* pv_last_error(void);
 
 /* Host buffers in, host bitmap out (ceil(n/8) bytes). sm_off has n+1 entries, non-decreasing;
- * offsets need no alignment (the library copies into its own pinned staging buffer). Synchronous. */
+ * offsets need no alignment (the library copies into its own pinned staging buffer). Synchronous.
+ * A call of <= 256 requests that takes the latency path, with records <= 1,840 bytes, is zero-copy:
+ * the requests go into fixed-stride slots of the pinned staging buffer that the kernel reads over
+ * PCIe, and each request's verdict byte is stored back into it (no copy kernels around the
+ * verification); with stage timing on or key-cache auto-admission active the host waits on the
+ * stream as for any other call. */
 int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
                     uint8_t* verdict_bits);
 

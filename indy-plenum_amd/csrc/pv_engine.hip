@@ -16,6 +16,8 @@
 #include <list>
 #include <unordered_map>
 #include <mutex>
+#include <chrono>
+#include <atomic>
 #include <random>
 #include <atomic>
 #include <condition_variable>
@@ -47,6 +49,12 @@ static constexpr int PV_BLOCK = 256;
 // [S]B of a keyed chunk per request from the chunk's start, beside the dedup (A/B knob, off): the
 // dedup's atomics slow 2-4x under it and the headline gains nothing measurable; config 3 loses
 // 0.1 ms (profiles/r03/half/ab_comb_b_early)
+#ifndef PV_ZERO_COPY  // small latency-path host-buffer calls read the pinned staging buffer in place
+#define PV_ZERO_COPY 1
+#endif
+#ifndef PV_ZC_SPIN  // ... and the host spins on their verdict bytes instead of a stream sync
+#define PV_ZC_SPIN 1
+#endif
 #ifndef PV_COMB_B_EARLY
 #define PV_COMB_B_EARLY 0
 #endif
@@ -1961,6 +1969,8 @@ int kc_upload_htab(hipStream_t s, uint32_t* hbuf = nullptr) {
     return PV_OK;
 }
 
+int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s);
+
 int ensure_stage(uint64_t host_bytes, uint64_t dev_bytes) {
     if (host_bytes > g_ctx.h_stage_cap) {
         if (g_ctx.h_stage) (void)hipHostFree(g_ctx.h_stage);
@@ -2705,6 +2715,76 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     for (uint64_t i = 0; i < n; i++)
         if (sm_off[i + 1] < sm_off[i]) return fail(PV_ERR_ARG, "sm_off must be non-decreasing");
     std::lock_guard<std::mutex> lk(g_mu);
+#if PV_ZERO_COPY
+    {
+        // a small call that takes the latency path (the same choice launch_chunks makes for a host-buffer
+        // call) and whose records fit a 2 KB slot: the kernel reads the pinned staging slots over PCIe
+        // and stores one verdict byte per request back -- no copy kernels around it
+        uint64_t maxlen = 0;
+        for (uint64_t i = 0; i < n && n <= PV_ZC_MAX_REQ; i++) maxlen = std::max(maxlen, sm_off[i + 1] - sm_off[i]);
+        const uint64_t stride = (4ull * PV_ZC_REC_WORD + maxlen + PV_ZC_SLACK + 63) & ~63ull;
+        if (!g_ctx.timing && n <= PV_ZC_MAX_REQ && stride <= PV_ZC_MAX_STRIDE &&
+            (g_ctx.path == PV_PATH_LATENCY ||
+             (g_ctx.path == PV_PATH_AUTO && n <= PV_LATENCY_MAX && !pv_keyed_hint(pk, n)))) {
+            const uint64_t vbytes = 256;  // >= PV_ZC_MAX_REQ
+            int rc = ensure_stage(vbytes + n * stride, 0);
+            if (rc) return rc;
+            uint8_t* vb = g_ctx.h_stage;
+            uint8_t* slots = g_ctx.h_stage + vbytes;
+            memset(vb, 0xFF, n);  // pending (PV_ZC_SPIN)
+            for (uint64_t i = 0; i < n; i++) {
+                uint8_t* sl = slots + i * stride;
+                const uint64_t len = sm_off[i + 1] - sm_off[i];
+                const uint32_t hdr[PV_ZC_PK_WORD] = {(uint32_t)len, 0u, 0u, 0u};
+                memcpy(sl, hdr, sizeof(hdr));
+                memcpy(sl + 4 * PV_ZC_PK_WORD, pk + 32 * i, 32);
+                memcpy(sl + 4 * PV_ZC_REC_WORD, sm + sm_off[i], len);
+                memset(sl + 4 * PV_ZC_REC_WORD + len, 0, stride - 4 * PV_ZC_REC_WORD - len);
+            }
+            hipStream_t s = g_ctx.stream;
+            if (g_ctx.last_stream && g_ctx.last_stream != s)
+                PV_HIP(hipStreamWaitEvent(s, g_ctx.ev_launch_done, 0), PV_ERR_LAUNCH);
+            g_ctx.last_latency = true;
+            g_ctx.last_keyed = false;
+            g_ctx.last_dev_choice = false;
+            rc = pv_latency_launch_zc(slots, (uint32_t)stride, n, g_ctx.d_bcomb, kc_view(), vb, s);
+            PV_HIP(hipEventRecord(g_ctx.ev_launch_done, s), PV_ERR_LAUNCH);
+            g_ctx.last_stream = s;
+            if (rc) {
+                (void)hipStreamSynchronize(s);
+                return rc;
+            }
+#if PV_ZC_SPIN
+            // the verdict bytes start at 0xFF and each workgroup's last store sets its byte: spin on
+            // them instead of the runtime's completion wait (a kernel fault still surfaces at the
+            // stream sync below or at the next call); bounded, then the ordinary wait
+            if (g_ctx.kc.auto_min == 0) {
+                const auto t0 = std::chrono::steady_clock::now();
+                volatile const uint8_t* vv = vb;
+                uint64_t i = 0;
+                while (i < n) {
+                    if (vv[i] != 0xFFu) {
+                        i++;
+                        continue;
+                    }
+                    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+                }
+                if (i == n) {
+                    std::atomic_thread_fence(std::memory_order_acquire);
+                    memset(verdict_bits, 0, (n + 7) / 8);
+                    for (uint64_t j = 0; j < n; j++) verdict_bits[j >> 3] |= (uint8_t)((vb[j] & 1u) << (j & 7));
+                    return PV_OK;
+                }
+            }
+#endif
+            rc = kc_auto_after_batch(pk, n, s);  // returns once the verdict bytes are written
+            if (rc) return rc;
+            memset(verdict_bits, 0, (n + 7) / 8);
+            for (uint64_t i = 0; i < n; i++) verdict_bits[i >> 3] |= (uint8_t)((vb[i] & 1u) << (i & 7));
+            return PV_OK;
+        }
+    }
+#endif
     // staging layout (one pinned buffer, one device buffer, 256-B aligned sections):
     //   [pk n*32][off (n+1) u64][verdict ceil(n/64) u64][blob + PV_BLOB_SLACK]
     auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
@@ -2762,9 +2842,18 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     if (rc) return rc;
     uint64_t* hver = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
     PV_HIP(hipMemcpyAsync(hver, dver, vwords * 8, hipMemcpyDeviceToHost, s), PV_ERR_LAUNCH);
-    // automatic key-cache admission: keys seen auto_min times get their tables built right behind
-    // this batch on the same stream; only the verdict copy is waited for, the build overlaps the
-    // caller's next steps (the next launch is ordered after it)
+    rc = kc_auto_after_batch(pk, n, s);
+    if (rc) return rc;
+    memcpy(verdict_bits, hver, (n + 7) / 8);  // little-endian words, LSB-first bits
+    return PV_OK;
+}
+
+namespace {
+// Automatic key-cache admission after a host-buffer batch whose verdicts are the last thing enqueued on
+// `s`: keys seen auto_min times get their tables built right behind the batch on the same stream; only
+// the verdicts are waited for, the build overlaps the caller's next steps (the next launch is ordered
+// after it). Returns once the verdicts are on the host.
+int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s) {
     auto& k = g_ctx.kc;
     std::vector<uint8_t> admit;
     if (k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken && n <= PV_KC_AUTO_MAX_BATCH) kc_auto_count(pk, n, admit);
@@ -2781,9 +2870,9 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     } else {
         PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
     }
-    memcpy(verdict_bits, hver, (n + 7) / 8);  // little-endian words, LSB-first bits
     return PV_OK;
 }
+}  // namespace
 
 int pv_comm_unique_id(uint8_t out[128]) {
     ncclUniqueId id;

@@ -104,3 +104,24 @@ def test_repeated_keys_with_adversarial(native, sodium, oracle):
     want = reference_verdicts(sodium, cases)
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
     assert 0.85 * len(cases) < want.sum() < len(cases)
+
+
+def test_small_calls_long_records(native, sodium, oracle):
+    """Small host-buffer calls (the latency path's zero-copy form in AUTO / LATENCY: the kernel reads the
+    pinned staging buffer and copies each record into LDS when it fits, else reads it in place) with
+    records around and beyond the LDS copy's size, valid and tampered, at every alignment."""
+    g = VectorGen(sodium, oracle, seed=16)
+    cases = []
+    for ln in list(range(1700, 1960, 20)) + [0, 1, 127, 128, 4000, 9000]:
+        sm, pk = g.valid(bytes(g.rng.getrandbits(8) for _ in range(ln)))
+        cases.append((sm, pk))
+        bad = bytearray(sm)
+        bad[-1 if ln else 0] ^= 0x10
+        cases.append((bytes(bad), pk))
+    blob, off, pks = pack(cases)
+    want = reference_verdicts(sodium, cases)
+    assert want.sum() == len(cases) // 2
+    for lead in (0, 1, 2, 3):
+        blob2 = np.concatenate([np.full(lead, 0x55, np.uint8), blob])
+        got = native.verify_sm_batch(blob2, off + lead, pks)
+        assert np.array_equal(got, want), (lead, np.nonzero(got != want)[0][:8])
