@@ -1969,7 +1969,7 @@ int kc_upload_htab(hipStream_t s, uint32_t* hbuf = nullptr) {
     return PV_OK;
 }
 
-int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s);
+int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s, const uint8_t* vb = nullptr);
 
 int ensure_stage(uint64_t host_bytes, uint64_t dev_bytes) {
     if (host_bytes > g_ctx.h_stage_cap) {
@@ -2754,30 +2754,7 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
                 (void)hipStreamSynchronize(s);
                 return rc;
             }
-#if PV_ZC_SPIN
-            // the verdict bytes start at 0xFF and each workgroup's last store sets its byte: spin on
-            // them instead of the runtime's completion wait (a kernel fault still surfaces at the
-            // stream sync below or at the next call); bounded, then the ordinary wait
-            if (g_ctx.kc.auto_min == 0) {
-                const auto t0 = std::chrono::steady_clock::now();
-                volatile const uint8_t* vv = vb;
-                uint64_t i = 0;
-                while (i < n) {
-                    if (vv[i] != 0xFFu) {
-                        i++;
-                        continue;
-                    }
-                    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
-                }
-                if (i == n) {
-                    std::atomic_thread_fence(std::memory_order_acquire);
-                    memset(verdict_bits, 0, (n + 7) / 8);
-                    for (uint64_t j = 0; j < n; j++) verdict_bits[j >> 3] |= (uint8_t)((vb[j] & 1u) << (j & 7));
-                    return PV_OK;
-                }
-            }
-#endif
-            rc = kc_auto_after_batch(pk, n, s);  // returns once the verdict bytes are written
+            rc = kc_auto_after_batch(pk, n, s, vb);  // returns once the verdict bytes are written
             if (rc) return rc;
             memset(verdict_bits, 0, (n + 7) / 8);
             for (uint64_t i = 0; i < n; i++) verdict_bits[i >> 3] |= (uint8_t)((vb[i] & 1u) << (i & 7));
@@ -2849,11 +2826,36 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
 }
 
 namespace {
+// Zero-copy verdict bytes start at 0xFF and each workgroup's last store sets its byte: the host spins
+// on them instead of the runtime's completion wait (a kernel fault surfaces at the next call's
+// synchronisation); bounded at 50 ms, then false and the caller waits on the stream.
+bool pv_spin_verdict_bytes(const uint8_t* vb, uint64_t n) {
+#if PV_ZC_SPIN
+    const auto t0 = std::chrono::steady_clock::now();
+    volatile const uint8_t* vv = vb;
+    uint64_t i = 0;
+    while (i < n) {
+        if (vv[i] != 0xFFu) {
+            i++;
+            continue;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) return false;
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return true;
+#else
+    (void)vb;
+    (void)n;
+    return false;
+#endif
+}
+
 // Automatic key-cache admission after a host-buffer batch whose verdicts are the last thing enqueued on
 // `s`: keys seen auto_min times get their tables built right behind the batch on the same stream; only
 // the verdicts are waited for, the build overlaps the caller's next steps (the next launch is ordered
-// after it). Returns once the verdicts are on the host.
-int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s) {
+// after it). Returns once the verdicts are on the host (vb: zero-copy verdict bytes, spun on when no key
+// is admitted).
+int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s, const uint8_t* vb) {
     auto& k = g_ctx.kc;
     std::vector<uint8_t> admit;
     if (k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken && n <= PV_KC_AUTO_MAX_BATCH) kc_auto_count(pk, n, admit);
@@ -2867,7 +2869,7 @@ int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s) {
             g_err = err;
         }
         PV_HIP(hipEventSynchronize(g_ctx.ev_verdict_copied), PV_ERR_LAUNCH);
-    } else {
+    } else if (!(vb && pv_spin_verdict_bytes(vb, n))) {
         PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
     }
     return PV_OK;
