@@ -2726,20 +2726,28 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
         if (!g_ctx.timing && n <= PV_ZC_MAX_REQ && stride <= PV_ZC_MAX_STRIDE &&
             (g_ctx.path == PV_PATH_LATENCY ||
              (g_ctx.path == PV_PATH_AUTO && n <= PV_LATENCY_MAX && !pv_keyed_hint(pk, n)))) {
-            const uint64_t vbytes = 256;  // >= PV_ZC_MAX_REQ
+            const uint64_t vbytes = PV_ZC_MAX_REQ;
             int rc = ensure_stage(vbytes + n * stride, 0);
             if (rc) return rc;
             uint8_t* vb = g_ctx.h_stage;
             uint8_t* slots = g_ctx.h_stage + vbytes;
             memset(vb, 0xFF, n);  // pending (PV_ZC_SPIN)
-            for (uint64_t i = 0; i < n; i++) {
-                uint8_t* sl = slots + i * stride;
-                const uint64_t len = sm_off[i + 1] - sm_off[i];
-                const uint32_t hdr[PV_ZC_PK_WORD] = {(uint32_t)len, 0u, 0u, 0u};
-                memcpy(sl, hdr, sizeof(hdr));
-                memcpy(sl + 4 * PV_ZC_PK_WORD, pk + 32 * i, 32);
-                memcpy(sl + 4 * PV_ZC_REC_WORD, sm + sm_off[i], len);
-                memset(sl + 4 * PV_ZC_REC_WORD + len, 0, stride - 4 * PV_ZC_REC_WORD - len);
+            auto fill = [&](uint64_t a, uint64_t b) {
+                for (uint64_t i = a; i < b; i++) {
+                    uint8_t* sl = slots + i * stride;
+                    const uint64_t len = sm_off[i + 1] - sm_off[i];
+                    const uint32_t hdr[PV_ZC_PK_WORD] = {(uint32_t)len, 0u, 0u, 0u};
+                    memcpy(sl, hdr, sizeof(hdr));
+                    memcpy(sl + 4 * PV_ZC_PK_WORD, pk + 32 * i, 32);
+                    memcpy(sl + 4 * PV_ZC_REC_WORD, sm + sm_off[i], len);
+                    memset(sl + 4 * PV_ZC_REC_WORD + len, 0, stride - 4 * PV_ZC_REC_WORD - len);
+                }
+            };
+            if (n * stride < (128u << 10)) {
+                fill(0, n);
+            } else {  // node-quota sizes: the slots are written by the copy pool's threads
+                const unsigned k = 8;
+                g_copy_pool.run(k, [&](unsigned t) { fill(n * t / k, n * (t + 1) / k); });
             }
             hipStream_t s = g_ctx.stream;
             if (g_ctx.last_stream && g_ctx.last_stream != s)

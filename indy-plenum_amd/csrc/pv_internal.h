@@ -19,14 +19,14 @@ struct PvKeyCacheView;
 int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk,
                       const void* d_bcomb, const PvKeyCacheView& kc, uint64_t* d_verdict, bool verdict_zeroed,
                       hipStream_t stream, const uint32_t* run_if);
-// Zero-copy latency path for a small host-buffer call: n <= PV_ZC_MAX_REQ requests in pinned host memory,
+// Zero-copy latency path for a host-buffer call of n <= PV_ZC_MAX_REQ requests in pinned host memory,
 // request r in the slot h_slots + r * stride: word 0 = smlen, words PV_ZC_PK_WORD.. the 32-byte key, the
 // record's bytes from word PV_ZC_REC_WORD, then >= PV_ZC_SLACK zero bytes (the hash reads ahead); stride a
 // multiple of 64, <= PV_ZC_MAX_STRIDE. The kernel reads the slots directly and stores one verdict byte
 // per request to h_vbytes (pinned host memory).
 int pv_latency_launch_zc(const uint8_t* h_slots, uint32_t stride, uint64_t n, const void* d_bcomb,
                          const PvKeyCacheView& kc, uint8_t* h_vbytes, hipStream_t stream);
-static constexpr uint64_t PV_ZC_MAX_REQ = 256;      // = PV_LAT4_MAX
+static constexpr uint64_t PV_ZC_MAX_REQ = 2048;     // = PV_LATENCY_MAX (four-wave form up to PV_LAT4_MAX)
 static constexpr uint32_t PV_ZC_MAX_STRIDE = 2048;  // bytes per slot (the LDS copy)
 static constexpr uint32_t PV_ZC_PK_WORD = 4, PV_ZC_REC_WORD = 12, PV_ZC_SLACK = 160;
 

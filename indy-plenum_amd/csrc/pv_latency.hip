@@ -63,11 +63,17 @@ struct LatMsg {
     }
 };
 
+[[maybe_unused]] constexpr uint32_t PV_ZC_MSG_WORDS = PV_ZC_MAX_STRIDE / 4;
+
+// ZC: zero-copy host-buffer call (pv_latency_launch_zc; slot layout and verdict bytes as in
+// pv_lat4_kernel below).
+template <bool ZC>
 __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __restrict__ sm,
                                                               const uint64_t* __restrict__ off, uint64_t n,
                                                               const uint8_t* __restrict__ pk,
                                                               const uint32_t* __restrict__ bcomb, PvKeyCacheView kc,
                                                               unsigned long long* __restrict__ verdict,
+                                                              uint8_t* __restrict__ vbytes, uint32_t zstride,
                                                               const uint32_t* __restrict__ run_if) {
 #if LP_DEVICE  // the lp types are 64-lane host arrays in the host pass: the body is device-only
     if (run_if && *run_if == 0u) return;  // AUTO's device-side choice picked the keyed path
@@ -81,22 +87,37 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
     __shared__ uint32_t s_sb[64];          // wave 1's result, ext layout, one word per lane
     __shared__ uint32_t s_tab[17][64];     // [j](-A), j = -8..8, cached layout
     __shared__ uint32_t s_rtab[17][64];    // [j]R', j = -8..8
+    __shared__ uint32_t s_msg[ZC ? PV_ZC_MSG_WORDS : 1];
 
-    const uint64_t o0 = off[r], o1 = off[r + 1];
-    const uint64_t smlen = o1 - o0;
-    const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
-    const LatMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+    uint64_t smlen;
+    const uint32_t* ap;
+    uint32_t sh;
     pv_sig_words in;
+    if constexpr (ZC) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(sm + (uint64_t)r * zstride);
+        for (uint32_t t = threadIdx.x; t < zstride / 4; t += LAT_THREADS) s_msg[t] = src[t];
+        __syncthreads();
+        smlen = s_msg[0];
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-        in.R[q] = mw.dw(q);
-        in.S[q] = mw.dw(8 + q);
-    }
-    {
+        for (int q = 0; q < 8; q++) in.A[q] = s_msg[PV_ZC_PK_WORD + q];
+        ap = s_msg + PV_ZC_REC_WORD;
+        sh = 0;
+    } else {
+        const uint64_t o0 = off[r], o1 = off[r + 1];
+        smlen = o1 - o0;
+        const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
+        ap = reinterpret_cast<const uint32_t*>(raddr & ~3ull);
+        sh = (uint32_t)(raddr & 3);
         const uint4* p4 = reinterpret_cast<const uint4*>(pk + 32 * (uint64_t)r);
         const uint4 a0 = p4[0], a1 = p4[1];
         in.A[0] = a0.x; in.A[1] = a0.y; in.A[2] = a0.z; in.A[3] = a0.w;
         in.A[4] = a1.x; in.A[5] = a1.y; in.A[6] = a1.z; in.A[7] = a1.w;
+    }
+    const LatMsg mw{ap, sh};
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        in.R[q] = mw.dw(q);
+        in.S[q] = mw.dw(8 + q);
     }
     const LpLane c = LpLane::make();
     const LpConsts K = LpConsts::make(c);
@@ -226,7 +247,11 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
     LAT_STAMP(5);
     const bool eq = lp_final_check(c, K, QA, s_sb[lane], dec.X, dec.Y);
     const bool ok = eq && key_ok && r_ok && s_sig_ok != 0;
-    if (lane == 0 && ok) atomicOr(&verdict[r >> 6], 1ull << (r & 63));
+    if constexpr (ZC) {
+        if (lane == 0) vbytes[r] = ok ? 1u : 0u;
+    } else {
+        if (lane == 0 && ok) atomicOr(&verdict[r >> 6], 1ull << (r & 63));
+    }
     LAT_STAMP(6);
 #endif
 }
@@ -252,7 +277,6 @@ constexpr int LAT4_THREADS = 256;
 // workgroup copies its slot into LDS in ONE PCIe round trip (no offset lookup first) and the verdict is
 // one byte per request stored to host memory (vbytes) instead of OR-ed into device words: no copy
 // kernels before or after the verification.
-[[maybe_unused]] constexpr uint32_t PV_ZC_MSG_WORDS = PV_ZC_MAX_STRIDE / 4;
 
 template <bool ZC>
 __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __restrict__ sm,
@@ -483,9 +507,9 @@ int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, co
                            d_pk, reinterpret_cast<const uint32_t*>(d_bcomb), kc,
                            reinterpret_cast<unsigned long long*>(d_verdict), nullptr, 0u, run_if);
     else
-        hipLaunchKernelGGL(pv_lat_kernel, dim3((unsigned)n), dim3(LAT_THREADS), 0, stream, d_sm, d_off, n, d_pk,
-                           reinterpret_cast<const uint32_t*>(d_bcomb), kc,
-                           reinterpret_cast<unsigned long long*>(d_verdict), run_if);
+        hipLaunchKernelGGL(pv_lat_kernel<false>, dim3((unsigned)n), dim3(LAT_THREADS), 0, stream, d_sm, d_off, n,
+                           d_pk, reinterpret_cast<const uint32_t*>(d_bcomb), kc,
+                           reinterpret_cast<unsigned long long*>(d_verdict), nullptr, 0u, run_if);
     e = hipGetLastError();
     if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("pv_lat_kernel: ") + hipGetErrorString(e));
     return PV_OK;
@@ -494,10 +518,14 @@ int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, co
 int pv_latency_launch_zc(const uint8_t* h_slots, uint32_t stride, uint64_t n, const void* d_bcomb,
                          const PvKeyCacheView& kc, uint8_t* h_vbytes, hipStream_t stream) {
     if (n == 0) return PV_OK;
-    if (n > PV_LAT4_MAX || n > PV_ZC_MAX_REQ) return pv_fail(PV_ERR_ARG, "pv_latency_launch_zc: too many requests");
+    if (n > PV_ZC_MAX_REQ) return pv_fail(PV_ERR_ARG, "pv_latency_launch_zc: too many requests");
     if (stride % 64 || stride > PV_ZC_MAX_STRIDE) return pv_fail(PV_ERR_ARG, "pv_latency_launch_zc: bad slot stride");
-    hipLaunchKernelGGL(pv_lat4_kernel<true>, dim3((unsigned)n), dim3(LAT4_THREADS), 0, stream, h_slots, nullptr, n,
-                       nullptr, reinterpret_cast<const uint32_t*>(d_bcomb), kc, nullptr, h_vbytes, stride, nullptr);
+    if (n <= PV_LAT4_MAX)
+        hipLaunchKernelGGL(pv_lat4_kernel<true>, dim3((unsigned)n), dim3(LAT4_THREADS), 0, stream, h_slots, nullptr, n,
+                           nullptr, reinterpret_cast<const uint32_t*>(d_bcomb), kc, nullptr, h_vbytes, stride, nullptr);
+    else
+        hipLaunchKernelGGL(pv_lat_kernel<true>, dim3((unsigned)n), dim3(LAT_THREADS), 0, stream, h_slots, nullptr, n,
+                           nullptr, reinterpret_cast<const uint32_t*>(d_bcomb), kc, nullptr, h_vbytes, stride, nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("pv_lat4_kernel<zc>: ") + hipGetErrorString(e));
     return PV_OK;

@@ -7,7 +7,7 @@ mkdir -p gpurun_out/ablat
 for round in 1 2; do
   for v in "$@"; do
     if [ "$v" = base ]; then unset PLENUM_AMD_LIB; else export PLENUM_AMD_LIB=variants/$v/libplenum_verify.so; fi
-    timeout -k 10 120 python3 tools/lat_breakdown.py run 300 > gpurun_out/ablat/$v.$round.json 2> gpurun_out/ablat/$v.$round.log || exit $?
+    timeout -k 10 120 python3 tools/lat_breakdown.py run 300 ${SIZES:-1,100} > gpurun_out/ablat/$v.$round.json 2> gpurun_out/ablat/$v.$round.log || exit $?
     echo "$v $(cat gpurun_out/ablat/$v.$round.json)"
   done
 done

@@ -1,6 +1,6 @@
 """Where the host-buffer latency of a small pv_verify_batch call goes (latency path, no stage events).
 
-    python tools/lat_breakdown.py run [--reps 300]          # the calls (run under rocprofv3 --kernel-trace
+    python tools/lat_breakdown.py run [REPS [SIZES]]        # the calls (run under rocprofv3 --kernel-trace
                                                             #   --memory-copy-trace), prints median host times
     python tools/lat_breakdown.py analyze TRACE_DB          # per call: ops on the GPU, durations and gaps (us)
 """
@@ -16,14 +16,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "indy-plenum_amd"), os.path.join(ROOT, "tools")]
 
 
-def run(reps):
+def run(reps, sizes=(1, 100)):
     import nym_workload
     from plenum_amd import _native
-    blob, off, pks = nym_workload.generate(0, 100, workers=4)
+    blob, off, pks = nym_workload.generate(0, max(sizes), workers=4)
     _native.ensure_device()
     _native.set_path(_native.PV_PATH_AUTO)
     out = {}
-    for n in (1, 100):
+    for n in sizes:
         o = off[:n + 1]
         b, p = blob[:int(o[-1])], pks[:n]
         for _ in range(20):
@@ -90,6 +90,7 @@ def analyze(db):
 
 if __name__ == "__main__":
     if sys.argv[1] == "run":
-        run(int(sys.argv[3]) if len(sys.argv) > 3 else 300)
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 300,
+            tuple(int(x) for x in sys.argv[3].split(",")) if len(sys.argv) > 3 else (1, 100))
     else:
         analyze(sys.argv[2])
