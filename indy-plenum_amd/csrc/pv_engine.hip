@@ -804,7 +804,23 @@ __device__ __forceinline__ uint32_t pv_key_hash(const uint32_t A[8], uint32_t se
 
 // Sub-table of request i's per-key counter: its workgroup of the insert / scatter / unpermute grids
 // (all PV_BLOCK requests per workgroup, request i in workgroup i / PV_BLOCK).
-__device__ __forceinline__ uint32_t pv_rank_sub(uint32_t i) { return (i / PV_BLOCK) & (PV_RANK_SUB - 1u); }
+// PV_INSERT_LDS: the insert kernel's workgroup takes PV_INS_REQS consecutive requests, counts their
+// keys in an LDS table and makes ONE device atomic per (key, workgroup) for the whole group's ranks
+// (the per-request atomics on the keys' counters were ~56 of the kernel's ~74 us at 1M requests);
+// the sub-table is then the request's insert-workgroup index mod PV_RANK_SUB.
+#ifndef PV_INSERT_LDS
+#define PV_INSERT_LDS 0
+#endif
+static constexpr uint32_t PV_INS_THREADS = 1024, PV_INS_PER_THREAD = 4;
+static constexpr uint32_t PV_INS_REQS = PV_INS_THREADS * PV_INS_PER_THREAD;
+static constexpr uint32_t PV_INS_LT = 4096;  // LDS table entries (more distinct keys: direct atomics)
+__device__ __forceinline__ uint32_t pv_rank_sub(uint32_t i) {
+#if PV_INSERT_LDS
+    return (i / PV_INS_REQS) & (PV_RANK_SUB - 1u);
+#else
+    return (i / PV_BLOCK) & (PV_RANK_SUB - 1u);
+#endif
+}
 
 // Dedup 1/2: open-addressing insert of every request's key; req_key[i] = the key's slot.
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* __restrict__ pk, uint64_t n,
@@ -838,7 +854,85 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_insert_kernel(const uint8_t* 
     kw.req_key[i] = h;
     // the request's rank among its key's requests, and (final after this kernel) the key's count;
     // the 1,024-odd counters of a batch sit on distinct hash slots, i.e. mostly distinct L2 lines
+#ifdef PV_AB_NO_RANK_ATOMIC  // measurement-only: wrong slot order
+    kw.req_rank[i] = 0u;
+    kw.slot_cnt[pv_rank_sub(i) * (kw.hmask + 1ull) + h] = 1u;
+#else
     kw.req_rank[i] = atomicAdd(&kw.slot_cnt[pv_rank_sub(i) * (kw.hmask + 1ull) + h], 1u);
+#endif
+}
+
+// The key's slot of request i (open addressing; the key is inserted if new), as pv_key_insert_kernel.
+__device__ __forceinline__ uint32_t pv_key_slot(const uint8_t* __restrict__ pk, const KeyWork& kw, uint32_t i) {
+    uint32_t A[8];
+    pv_load_pk(A, pk, i);
+    uint32_t h = pv_key_hash(A, kw.seed) & kw.hmask;
+    for (uint32_t probe = 0; probe <= kw.hmask; probe++) {  // the table is >= 2x the chunk: never full
+#if PV_INSERT_PLAIN_LOAD
+        uint32_t cur = kw.slot[h];
+#else
+        uint32_t cur = __hip_atomic_load(&kw.slot[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        if (cur == PV_EMPTY) cur = atomicCAS(&kw.slot[h], PV_EMPTY, i);
+        if (cur == PV_EMPTY) break;
+        uint32_t B[8];
+        pv_load_pk(B, pk, cur);
+        if (pv_words_equal(A, B)) break;
+        h = (h + 1) & kw.hmask;
+    }
+    return h;
+}
+
+// Dedup 1/2, LDS-aggregated form (PV_INSERT_LDS): every request's key slot as above, then its rank
+// among the key's requests = the workgroup's base for the key (one device atomic per distinct key of
+// the workgroup) + its rank inside the workgroup (an LDS atomic).
+__global__ __launch_bounds__(PV_INS_THREADS) void pv_key_insert_lds_kernel(const uint8_t* __restrict__ pk, uint64_t n,
+                                                                          KeyWork kw) {
+    __shared__ uint32_t lkey[PV_INS_LT], lcnt[PV_INS_LT];
+    const uint32_t t = threadIdx.x;
+    const uint32_t g = blockIdx.x * PV_INS_THREADS + t;
+    if (g < PV_SPLIT_WORDS) kw.nkeys[g] = 0u;  // the chunk's split counters (see pv_key_insert_kernel)
+    if (g < PV_NSEG) kw.nkeys[PV_SEG_BASE + g * PV_SEG_STRIDE] = 0u;
+    for (uint32_t e = t; e < PV_INS_LT; e += PV_INS_THREADS) {
+        lkey[e] = PV_EMPTY;
+        lcnt[e] = 0u;
+    }
+    __syncthreads();
+    const uint32_t i0 = blockIdx.x * PV_INS_REQS;
+    uint32_t* cnt = kw.slot_cnt + (uint64_t)((blockIdx.x & (PV_RANK_SUB - 1u))) * (kw.hmask + 1ull);
+    uint32_t hs[PV_INS_PER_THREAD], es[PV_INS_PER_THREAD], lr[PV_INS_PER_THREAD];
+#pragma unroll
+    for (uint32_t u = 0; u < PV_INS_PER_THREAD; u++) {
+        const uint32_t i = i0 + u * PV_INS_THREADS + t;
+        es[u] = PV_EMPTY;
+        if (i >= n) continue;
+        const uint32_t h = pv_key_slot(pk, kw, i);
+        hs[u] = h;
+        kw.req_key[i] = h;
+        uint32_t e = (h * 2654435761u) >> (32 - 12);  // log2(PV_INS_LT)
+        for (int probe = 0; probe < 64; probe++) {
+            const uint32_t cur = atomicCAS(&lkey[e], PV_EMPTY, h);
+            if (cur == PV_EMPTY || cur == h) {
+                es[u] = e;
+                break;
+            }
+            e = (e + 1) & (PV_INS_LT - 1u);
+        }
+        if (es[u] != PV_EMPTY) lr[u] = atomicAdd(&lcnt[e], 1u);
+        else lr[u] = atomicAdd(&cnt[h], 1u);  // LDS table crowded: this request counts itself
+    }
+    __syncthreads();
+    for (uint32_t e = t; e < PV_INS_LT; e += PV_INS_THREADS) {
+        const uint32_t h = lkey[e];
+        if (h != PV_EMPTY) lcnt[e] = atomicAdd(&cnt[h], lcnt[e]);  // count -> the workgroup's base
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < PV_INS_PER_THREAD; u++) {
+        const uint32_t i = i0 + u * PV_INS_THREADS + t;
+        if (i >= n) continue;
+        kw.req_rank[i] = es[u] != PV_EMPTY ? lcnt[es[u]] + lr[u] : lr[u];
+    }
 }
 
 // Dedup 0/2: the first requests of the chunk claim their keys' slots before the full insert, so a
@@ -2128,7 +2222,12 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                                    stream, d_pk + 32 * c0, ms, kw);
                 PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             }
+#if PV_INSERT_LDS
+            hipLaunchKernelGGL(pv_key_insert_lds_kernel, dim3((unsigned)((m + PV_INS_REQS - 1) / PV_INS_REQS)),
+                               dim3(PV_INS_THREADS), 0, stream, d_pk + 32 * c0, m, kw);
+#else
             hipLaunchKernelGGL(pv_key_insert_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0, m, kw);
+#endif
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #if PV_COMB_B_EARLY
             if (PV_COMB_B_AFTER == 1 && (rc = launch_b_early())) return rc;

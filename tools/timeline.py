@@ -29,11 +29,11 @@ def main():
     q = next((c for c in ("stream_id", "queue_id", "queue") if c in cols), None)
     sel = "select name, start, end%s from kernels order by start" % (", " + q if q else "")
     rows = [(short(r[0]), int(r[1]), int(r[2]), r[3] if q else "") for r in con.execute(sel)]
-    starts = [i for i, r in enumerate(rows) if r[0] == a.first_kernel]
+    starts = [i for i, r in enumerate(rows) if r[0].startswith(a.first_kernel)]  # also pv_key_insert_lds_kernel
     if not starts:
         raise SystemExit("no %s in the trace (columns: %s)" % (a.first_kernel, cols))
     if a.summary:
-        keys = ("pv_key_assign_kernel", "pv_key_scan_kernel", "pv_key_chain_lp_kernel", "pv_key_fill_kernel",
+        keys = ("pv_key_insert", "pv_key_assign_kernel", "pv_key_scan_kernel", "pv_key_chain_lp_kernel", "pv_key_fill_kernel",
                 "pv_comb_b_kernel", "pv_comb_a_kernel", "pv_msm_kernel", "pv_encode_kernel")
         print("row    span   " + " ".join("%8s" % k.replace("pv_", "").replace("_kernel", "")[:8] for k in keys)
               + "  comb_a_start")
@@ -45,7 +45,7 @@ def main():
             ca = 0.0
             for name, st, en, _ in rows[s:nxt]:
                 for k in keys:
-                    if name.endswith(k) or name.startswith("void " + k):
+                    if name.endswith(k) or name.startswith(k) or name.startswith("void " + k):
                         dur[k] = dur.get(k, 0.0) + (en - st) / 1e3
                 if "pv_comb_a_kernel" in name:
                     ca = (st - t0) / 1e3
