@@ -1005,6 +1005,33 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_cache_probe_kernel(const uint
 }
 
 // Exclusive prefix sum of one value per thread over a 1024-thread workgroup; *total = the sum.
+#ifndef PV_SCAN_WAVE
+#define PV_SCAN_WAVE 0
+#endif
+#if PV_SCAN_WAVE
+// Wave scans by shuffles, then the 16 wave totals (two barriers instead of Hillis-Steele's twenty).
+__device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint32_t x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    __syncthreads();  // every thread is done with the previous scan's results
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) {
+        const uint32_t pw = part[u];
+        before += u < w ? pw : 0u;
+        all += pw;
+    }
+    *total = all;
+    return before + x - v;
+}
+#else
 __device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
     const uint32_t t = threadIdx.x;
     __syncthreads();  // every thread is done with the previous scan's results
@@ -1019,6 +1046,7 @@ __device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
     *total = part[1023];
     return t ? part[t - 1] : 0u;
 }
+#endif
 
 // Sort 2/3 (one workgroup): split the keys between the paths and give each key its slot range.
 // Comb keys (>= min_req requests, the first kcap of them in id order) take slots [0, CS) in id
