@@ -809,7 +809,7 @@ __device__ __forceinline__ uint32_t pv_key_hash(const uint32_t A[8], uint32_t se
 // (the per-request atomics on the keys' counters were ~56 of the kernel's ~74 us at 1M requests);
 // the sub-table is then the request's insert-workgroup index mod PV_RANK_SUB.
 #ifndef PV_INSERT_LDS
-#define PV_INSERT_LDS 0
+#define PV_INSERT_LDS 1
 #endif
 static constexpr uint32_t PV_INS_THREADS = 1024, PV_INS_PER_THREAD = 4;
 static constexpr uint32_t PV_INS_REQS = PV_INS_THREADS * PV_INS_PER_THREAD;
@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_cache_probe_kernel(const uint
 
 // Exclusive prefix sum of one value per thread over a 1024-thread workgroup; *total = the sum.
 #ifndef PV_SCAN_WAVE
-#define PV_SCAN_WAVE 0
+#define PV_SCAN_WAVE 1
 #endif
 #if PV_SCAN_WAVE
 // Wave scans by shuffles, then the 16 wave totals (two barriers instead of Hillis-Steele's twenty).

@@ -19,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--first-kernel", default="pv_key_insert_kernel")
+    ap.add_argument("--first-kernel", default="pv_key_insert")
     ap.add_argument("--summary", action="store_true",
                     help="one line per step of the whole trace: span and the main kernels' durations (us)")
     a = ap.parse_args()
