@@ -497,6 +497,131 @@ def config3_leg(db_like, blob0, off, pks, steps, warmup, timed_fn):
     return res, got, (blob3, off, pks3)
 
 
+def workload_name(n, world):
+    return ("configs[1]: %d single-sig NYM-style requests (~299 B signing-serialized, 1024 signer DIDs)" % n
+            if world == 1 else
+            "configs[4]: %d single-sig NYM-style requests sharded over %d GPUs (%d per GPU, contiguous "
+            "64-aligned shards), verdict bitmaps all-gathered with RCCL every step" % (n * world, world, n))
+
+
+def assemble_result(world, n, steps, warmup, elapsed, stage_ms, chunks, comb, nkeys, record_bytes_avg,
+                    ok_local, ok_all, per_gpu_fixed=False):
+    """The headline bench line from the measured quantities (every rank count; the optional legs are
+    added by the caller): value = requests of all ranks / the max-over-ranks time of `steps` steps,
+    the roofline of the dominant kernel from its HIP-event launch time (stage "msm" / chunks), the
+    whole-pipeline figures from the stage times."""
+    total = n * world * steps
+    value = total / elapsed
+    ms_per_step = 1e3 * elapsed / steps
+    mac_kernel = BC.MAC_COMB_MSM_KERNEL if comb else BC.MAC_MSM_HALF_KERNEL
+    launch_ms = stage_ms["msm"] / chunks  # the roofline kernel's average launch (one per chunk)
+    achieved = mac_kernel * (n / chunks) / (launch_ms * 1e-3)
+    pipeline_ms = sum(stage_ms.values())
+    per_gpu_rate = n / (pipeline_ms * 1e-3)
+    mac_executed = (BC.MAC_COMB_MSM + BC.MAC_ENCODE / 4 + BC.MAC_COMB_PER_KEY * nkeys / (n / chunks)) if comb \
+        else (BC.MAC_PER_VERIFY - BC.MAC_ENCODE * 3 / 4)
+    kernel = "pv_comb_a_kernel" if comb else "pv_msm_kernel"
+    return {
+        "metric": METRIC, "value": round(value, 1), "unit": "verifies/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "weak" if world == 1 or per_gpu_fixed else "strong",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": workload_name(n, world) + ", %d of them tampered (must-reject), device-resident" % (
+                       tamper_count(n) * world),
+                   "requests_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
+                   "chunks_per_gpu_step": chunks, "record_bytes_avg": round(record_bytes_avg, 1),
+                   "path": "keyed comb (%d distinct keys per chunk, tables built inside every step)" % nkeys if comb
+                   else "per-request Straus"},
+        "roofline": {"bound": "valu", "kernel": kernel,
+                     "achieved": round(achieved / 1e12, 3), "peak": round(BC.PEAK_MAC_PER_S / 1e12, 3),
+                     "unit": "TMAC/s (v_mad_u64_u32 int32 MACs)", "frac": round(achieved / BC.PEAK_MAC_PER_S, 4),
+                     "traffic": pmc_traffic(kernel),
+                     "algorithmic_mac_per_verify": round(mac_kernel), "launch_ms": round(launch_ms, 4),
+                     "frac_of_measured_mad_stream": round(achieved / BC.MEASURED_MAD_STREAM_MAC_PER_S, 4),
+                     "valu_issue_per_cu_cycle_pmc": pmc_valu_issue(kernel)},
+        "pipeline": {**{s + "_ms": round(v, 4) for s, v in stage_ms.items()},
+                     "kernel_verifies_per_s_per_gpu": round(per_gpu_rate, 1),
+                     "whole_pipeline_valu_frac": round(mac_executed * per_gpu_rate / BC.PEAK_MAC_PER_S, 4),
+                     "libsodium_equivalent_mac_rate_over_peak": round(
+                         BC.MAC_PER_VERIFY * per_gpu_rate / BC.PEAK_MAC_PER_S, 4),
+                     "hbm_staging_GBps": round(BC.ALGO_BYTES_PER_VERIFY * per_gpu_rate / 1e9, 2),
+                     "note": "stage times (and the roofline kernel's launch time) from a second timed run with "
+                             "stage-boundary events on the stream; value / ms_per_step from the run without them"},
+        "verdicts_ok": bool(ok_local and (ok_all is None or ok_all)),
+        "verdicts_check": "bitmap == known bits (valid except %d tampered records per GPU)%s" % (
+            tamper_count(n), ", all %d shards' gathered bitmaps checked on every rank" % world if world > 1 else ""),
+    }
+
+
+def add_cpu_baseline(result, cb, c1=None):
+    """Attach the libsodium CPU path timed on this box's host cores (rank 0, same run) to the line."""
+    result["cpu_baseline"] = cb
+    result["vs_cpu_baseline"] = round(result["value"] / cb["value"], 1) if cb.get("value") else None
+    if c1:
+        result["cpu_baseline"]["config1_python_authenticate"] = c1
+    return result
+
+
+class FileBarrier:
+    """Host-side wait of ranks 1..N-1 while rank 0 runs a leg of its own (the CPU baseline, the
+    single-process multi-GPU leg): a file per tag, polled with sleeps, so the waiting ranks spin
+    neither a GPU collective nor a host core beside the leg being timed."""
+
+    def __init__(self, world, rank):
+        import tempfile
+        self.world, self.rank = world, rank
+        job = os.environ.get("PV_BENCH_JOB") or "%d_%s" % (os.getppid(), os.environ.get("MASTER_PORT", "0"))
+        self.base = os.path.join(tempfile.gettempdir(), "pv_bench_%s" % job)
+        self.made = []
+
+    def release(self, tag):
+        if self.rank == 0:
+            p = "%s.%s.done" % (self.base, tag)
+            with open(p, "w") as f:
+                f.write("1")
+            self.made.append(p)
+
+    def wait(self, tag, timeout_s=1200):
+        if self.rank == 0:
+            return
+        p = "%s.%s.done" % (self.base, tag)
+        t0 = time.time()
+        while not os.path.exists(p):
+            if time.time() - t0 > timeout_s:
+                raise TimeoutError("rank %d: rank 0's %s leg did not finish in %d s" % (self.rank, tag, timeout_s))
+            time.sleep(0.05)
+
+    def cleanup(self):
+        for p in self.made:
+            try:
+                os.remove(p)
+            except OSError:
+                pass
+
+
+def single_process_leg(blob, off, pks, want, world):
+    """pv_verify_batch_multi_gpu from ONE process over the node's `world` GPUs (rank 0, while the other
+    ranks wait): this rank's shard, host buffers in, sharded over every device with one in-process RCCL
+    all-gather (the path a Plenum node process would use). Secondary, never `value`."""
+    t0 = time.perf_counter()
+    devs = _native.ensure_devices(range(world))
+    init_s = time.perf_counter() - t0
+    n = len(off) - 1
+    _native.verify_sm_batch_multi(blob, off, pks, devs)  # warm: staging buffers sized on every device
+    ts, ok = [], True
+    for _ in range(3):
+        t1 = time.perf_counter()
+        got = _native.verify_sm_batch_multi(blob, off, pks, devs)
+        ts.append(time.perf_counter() - t1)
+        ok &= bool(np.array_equal(got, want))
+    med = float(np.median(ts))
+    return {"devices": list(devs), "requests": n, "verifies_per_s": round(n / med, 1), "seconds": round(med, 4),
+            "init_devices_s": round(init_s, 2), "ok": ok,
+            "note": "pv_verify_batch_multi_gpu: host buffers, one worker thread per device (pinned staging + "
+                    "H2D + verification on its own stream), one in-process ncclAllGather of the verdict words, "
+                    "PCIe included; median of 3 calls"}
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -584,6 +709,8 @@ def main():
     ap.add_argument("--dataset", default=None, help="npz from tools/nym_workload.py (profiling runs: no fork)")
     ap.add_argument("--no-ingress", action="store_true", help="skip the ingress / host-serialization measurements")
     ap.add_argument("--no-multisig", action="store_true", help="skip the configs[3] multi-signature measurement")
+    ap.add_argument("--no-single-process", action="store_true",
+                    help="N > 1: skip rank 0's pv_verify_batch_multi_gpu leg over every GPU of the node")
     ap.add_argument("--rank-stub", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -616,11 +743,7 @@ def main():
         n = 1 << 20
     else:  # configs[4]: the 64M-request batch sharded over the N GPUs (64-aligned shards)
         n = (CONFIG5_TOTAL + world * 64 - 1) // (world * 64) * 64
-    workload = ("configs[1]: %d single-sig NYM-style requests (~299 B signing-serialized, 1024 signer DIDs)" % n
-                if world == 1 else
-                "configs[4]: %d single-sig NYM-style requests sharded over %d GPUs (%d per GPU, contiguous "
-                "64-aligned shards), verdict bitmaps all-gathered with RCCL every step" % (n * world, world, n))
-
+    phases = {}  # per-phase wall budget (stderr and the line's "phases_s")
     t0 = time.perf_counter()
     wire = None
     if args.dataset and os.path.exists(args.dataset):
@@ -635,13 +758,16 @@ def main():
         workers = min(64, max(16, cores // world)) if world > 1 else None
         blob0, off, pks = nym_workload.generate(rank * n, n, workers=workers)
     gen_s = time.perf_counter() - t0
+    phases["generation"] = gen_s
     log("rank %d: generated %d requests (%.1f MB) in %.1f s" % (rank, n, blob0.nbytes / 1e6, gen_s))
     # the headline batch carries must-reject records: ~0.1 % of messages with one flipped byte
     import adversarial_batch
     blob, tampered = adversarial_batch.tamper(blob0, off, tamper_count(n), seed=1000 + rank)
     c1 = None
     if world == 1 and wire and not args.no_cpu_baseline:
+        t0 = time.perf_counter()
         c1 = config1_legs(wire)  # CPU leg, forked workers: before the device comes up
+        phases["config1_cpu_leg"] = time.perf_counter() - t0
     multi = None
     if world == 1 and not args.no_multisig and not args.dataset:
         t0 = time.perf_counter()
@@ -654,13 +780,14 @@ def main():
     t0 = time.perf_counter()
     _native.ensure_device(local_rank)
     L = _native.lib()
-    log("rank %d: device %d up (pv_init) in %.1f s" % (rank, local_rank, time.perf_counter() - t0))
+    phases["pv_init"] = time.perf_counter() - t0
+    log("rank %d: device %d up (pv_init) in %.1f s" % (rank, local_rank, phases["pv_init"]))
     t0 = time.perf_counter()
     db = DeviceBatch(blob, off, pks)
     comm = Comm(world, rank, L) if world > 1 else None
     d_all = db._alloc(db.words * 8 * world) if world > 1 else None
-    log("rank %d: batch uploaded%s in %.1f s" % (rank, " and communicator up" if comm else "",
-                                                 time.perf_counter() - t0))
+    phases["upload"] = time.perf_counter() - t0
+    log("rank %d: batch uploaded%s in %.1f s" % (rank, " and communicator up" if comm else "", phases["upload"]))
 
     def step():
         db.verify()
@@ -700,12 +827,13 @@ def main():
     for _ in range(args.warmup):
         step()
     _native.check(L.pv_sync(), "pv_sync")
-    log("rank %d: %d warm-up steps in %.1f s" % (rank, args.warmup, time.perf_counter() - t0))
+    phases["warmup"] = time.perf_counter() - t0
+    log("rank %d: %d warm-up steps in %.1f s" % (rank, args.warmup, phases["warmup"]))
     t0 = time.perf_counter()
     elapsed, _ = timed(args.steps, stages=False)  # the headline: no stage events in the measured loop
     _, stage_ms = timed(args.steps)                # stage breakdown and the roofline kernel's launch time
-    log("rank %d: timed runs in %.1f s (headline %.3f s for %d steps)" % (rank, time.perf_counter() - t0,
-                                                                        elapsed, args.steps))
+    phases["timed"] = time.perf_counter() - t0
+    log("rank %d: timed runs in %.1f s (headline %.3f s for %d steps)" % (rank, phases["timed"], elapsed, args.steps))
     chunks = timed.chunks
     path, nkeys = _native.last_path()
     comb = path == _native.PV_PATH_COMB
@@ -720,47 +848,8 @@ def main():
         allw = db.verdict_words(d_all, db.words * world).reshape(world, db.words)
         ok_all = all(np.array_equal(bits(allw[r], n), expected_bits(n, r)) for r in range(world))
 
-    total = n * world * args.steps
-    value = total / elapsed
-    ms_per_step = 1e3 * elapsed / args.steps
-    mac_kernel = BC.MAC_COMB_MSM_KERNEL if comb else BC.MAC_MSM_HALF_KERNEL
-    launch_ms = stage_ms["msm"] / chunks  # the roofline kernel's average launch (one per chunk)
-    achieved = mac_kernel * (n / chunks) / (launch_ms * 1e-3)
-    pipeline_ms = sum(stage_ms.values())
-    per_gpu_rate = n / (pipeline_ms * 1e-3)
-    mac_executed = (BC.MAC_COMB_MSM + BC.MAC_ENCODE / 4 + BC.MAC_COMB_PER_KEY * nkeys / (n / chunks)) if comb \
-        else (BC.MAC_PER_VERIFY - BC.MAC_ENCODE * 3 / 4)
-
-    result = {
-        "metric": METRIC, "value": round(value, 1), "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "weak" if world == 1 or args.per_gpu else "strong",
-        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-        "config": {"workload": workload + ", %d of them tampered (must-reject), device-resident" % (
-                       tamper_count(n) * world),
-                   "requests_per_gpu": n, "global_batch": n * world, "parallelism": "dp%d" % world,
-                   "chunks_per_gpu_step": chunks, "record_bytes_avg": round(float(blob.nbytes) / n, 1),
-                   "path": "keyed comb (%d distinct keys per chunk, tables built inside every step)" % nkeys if comb
-                   else "per-request Straus"},
-        "roofline": {"bound": "valu", "kernel": "pv_comb_a_kernel" if comb else "pv_msm_kernel",
-                     "achieved": round(achieved / 1e12, 3), "peak": round(BC.PEAK_MAC_PER_S / 1e12, 3),
-                     "unit": "TMAC/s (v_mad_u64_u32 int32 MACs)", "frac": round(achieved / BC.PEAK_MAC_PER_S, 4),
-                     "traffic": pmc_traffic("pv_comb_a_kernel" if comb else "pv_msm_kernel"),
-                     "algorithmic_mac_per_verify": round(mac_kernel), "launch_ms": round(launch_ms, 4),
-                     "frac_of_measured_mad_stream": round(achieved / BC.MEASURED_MAD_STREAM_MAC_PER_S, 4),
-                     "valu_issue_per_cu_cycle_pmc": pmc_valu_issue("pv_comb_a_kernel" if comb else "pv_msm_kernel")},
-        "pipeline": {**{s + "_ms": round(v, 4) for s, v in stage_ms.items()},
-                     "kernel_verifies_per_s_per_gpu": round(per_gpu_rate, 1),
-                     "whole_pipeline_valu_frac": round(mac_executed * per_gpu_rate / BC.PEAK_MAC_PER_S, 4),
-                     "libsodium_equivalent_mac_rate_over_peak": round(
-                         BC.MAC_PER_VERIFY * per_gpu_rate / BC.PEAK_MAC_PER_S, 4),
-                     "hbm_staging_GBps": round(BC.ALGO_BYTES_PER_VERIFY * per_gpu_rate / 1e9, 2),
-                     "note": "stage times (and the roofline kernel's launch time) from a second timed run with "
-                             "stage-boundary events on the stream; value / ms_per_step from the run without them"},
-        "verdicts_ok": ok_local and (ok_all is None or ok_all),
-        "verdicts_check": "bitmap == known bits (valid except %d tampered records per GPU)%s" % (
-            tamper_count(n), ", all %d shards' gathered bitmaps checked on every rank" % world if world > 1 else ""),
-    }
+    result = assemble_result(world, n, args.steps, args.warmup, elapsed, stage_ms, chunks, comb, nkeys,
+                             float(blob.nbytes) / n, ok_local, ok_all, per_gpu_fixed=bool(args.per_gpu))
     if world > 1 and not args.no_host_path:
         # SURVEY.md §8e host traffic: each rank's shard from host buffers (pv_verify_batch: pinned
         # staging pipelined with the H2D DMA, kernels, verdicts back), on up to configs[4]'s 8M-request
@@ -910,21 +999,41 @@ def main():
         result["multisig"] = multisig_leg(multi, min(n, 1 << 20), 3, max(3, args.steps // 4))
     if rank == 0 and world == 1 and wire:
         result["ingress"] = ingress_leg(n, blob0, off, wire, max(3, args.steps // 4), 1)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, c3_want = cpu_baseline(blob0, off, pks, min(args.cpu_sample, n), args.cpu_seconds,
-                                   config3=c3_batch if c3 else None)
-        result["cpu_baseline"] = cb
-        result["vs_cpu_baseline"] = round(value / cb["value"], 1)
-        if c1:
-            result["cpu_baseline"]["config1_python_authenticate"] = c1
-        if c3 is not None:
-            c3["verdicts_match_libsodium"] = bool(np.array_equal(c3_got, c3_want))
-            c3["mismatches"] = int((c3_got != c3_want).sum())
+    # rank 0's own legs at N > 1 (the other ranks wait on a file, idle): the single-process multi-GPU
+    # entry over every GPU of the node, then the CPU baseline on the node's host cores -- each in a
+    # try/except so that a failure records an error and never costs the headline line
+    fb = FileBarrier(world, rank) if world > 1 else None
+    if rank == 0 and world > 1 and not args.no_single_process:
+        t0 = time.perf_counter()
+        try:
+            result["single_process"] = single_process_leg(blob, off, pks, want_local, world)
+        except Exception as ex:
+            result["single_process"] = {"error": repr(ex)[:300]}
+        phases["single_process_leg"] = time.perf_counter() - t0
+    if rank == 0 and not args.no_cpu_baseline:
+        t0 = time.perf_counter()
+        try:
+            cb, c3_want = cpu_baseline(blob0, off, pks, min(args.cpu_sample, n), args.cpu_seconds,
+                                       config3=c3_batch if c3 else None)
+            add_cpu_baseline(result, cb, c1)
+            if c3 is not None:
+                c3["verdicts_match_libsodium"] = bool(np.array_equal(c3_got, c3_want))
+                c3["mismatches"] = int((c3_got != c3_want).sum())
+        except Exception as ex:
+            result["cpu_baseline"] = {"error": repr(ex)[:300]}
+        phases["cpu_baseline"] = time.perf_counter() - t0
+    if fb:
+        fb.release("rank0_legs")
+        fb.wait("rank0_legs")
     if rank == 0:
+        result["phases_s"] = {k: round(v, 2) for k, v in phases.items()}
+        log("rank 0: phase budget (s): " + ", ".join("%s %.1f" % kv for kv in phases.items()))
         print(json.dumps(result), flush=True)
     db.free()
     if comm:
         comm.close()
+    if fb:
+        fb.cleanup()
 
 
 if __name__ == "__main__":

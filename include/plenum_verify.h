@@ -25,8 +25,15 @@
  *   pv_comm_* / pv_allgather_verdicts
  *                          new: the cross-GPU gather of per-shard verdict bitmaps (one RCCL
  *                          all-gather over xGMI). The reference has no equivalent.
+ *   pv_init_devices / pv_verify_batch_multi_gpu
+ *                          the same batched crypto_sign_open as pv_verify_batch, sharded over several
+ *                          GPUs driven from ONE process (the reference's node is one process with one
+ *                          asyncio Looper, stp_core/loop/looper.py:142-213, fed from
+ *                          plenum/server/node.py:1518-1527 and stp_zmq/zstack.py:606-646), the
+ *                          per-shard verdict bitmaps gathered with one in-process RCCL all-gather.
  * Threading: the reference caller is the single-threaded asyncio Looper (stp_core/loop/looper.py);
- * the library is synchronous per call and keeps one context per process (one GPU per process).
+ * the library is synchronous per call. It keeps one context per device: pv_init binds the primary
+ * device that every single-device call uses; pv_init_devices adds contexts for the multi-GPU call.
  */
 #ifndef PLENUM_VERIFY_H
 #define PLENUM_VERIFY_H
@@ -65,13 +72,39 @@ const char* pv_last_error(void);
 
 /* Host buffers in, host bitmap out (ceil(n/8) bytes). sm_off has n+1 entries, non-decreasing;
  * offsets need no alignment (the library copies into its own pinned staging buffer). Synchronous.
- * A call of <= 256 requests that takes the latency path, with records <= 1,840 bytes, is zero-copy:
- * the requests go into fixed-stride slots of the pinned staging buffer that the kernel reads over
- * PCIe, and each request's verdict byte is stored back into it (no copy kernels around the
- * verification); with stage timing on or key-cache auto-admission active the host waits on the
- * stream as for any other call. */
+ * A call of <= 2,048 requests that takes the latency path (AUTO's range for host buffers without a
+ * key-repeat hint, or PV_PATH_LATENCY) and whose records are all <= 1,840 bytes is zero-copy: the
+ * requests go into fixed-stride slots of the pinned staging buffer that the kernel reads over PCIe,
+ * and each request's verdict byte is stored back into coherent pinned memory (no copy kernels around
+ * the verification); the host returns as soon as every byte is written (a fault of such a call is
+ * reported by the next call's synchronisation). With stage timing on or key-cache auto-admission
+ * active the host waits on the stream as for any other call. pv_last_zero_copy() returns 1 if the
+ * most recent pv_verify_batch took the zero-copy form. */
 int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
                     uint8_t* verdict_bits);
+int pv_last_zero_copy(void);
+
+/* Several GPUs from one process (SURVEY.md §8b pv_init(device_mask) / pv_verify_batch_multi_gpu).
+ *   pv_init_devices(mask)       bit d set = use device d (d < 16); builds each missing device context
+ *                               (tables, workspace, streams; in parallel) and one RCCL communicator per
+ *                               device with ncclCommInitAll. A primary bound by pv_init may be in the
+ *                               mask: its context is shared. Calling it again with another mask
+ *                               rebuilds the communicators only.
+ *   pv_verify_batch_multi_gpu   pv_verify_batch's contract (host buffers, synchronous, same verdict
+ *                               bits), sharded over those devices: shard r = requests
+ *                               [bounds[r], bounds[r+1]) of pv_shard_plan (contiguous, whole 64-request
+ *                               verdict words), staged and verified on device r's own stream by one host
+ *                               worker per device; the per-shard verdict words are gathered with ONE
+ *                               ncclAllGather over the clique (group call) and copied back from the first
+ *                               device. No other cross-GPU traffic.
+ *   pv_multi_gpu_devices        the devices in use (up to max), returns their count (0 = none).
+ *   pv_shard_plan               host-only: the shard bounds (ndev + 1 entries) and the verdict words
+ *                               per shard (the all-gather's count) for n requests over ndev devices. */
+int pv_init_devices(uint32_t device_mask);
+int pv_verify_batch_multi_gpu(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
+                              uint8_t* verdict_bits);
+int pv_multi_gpu_devices(int* devices, int max_devices);
+int pv_shard_plan(uint64_t n, int ndev, uint64_t* bounds, uint64_t* words_per_shard);
 
 /* Device buffers in, device bitmap out. Requirements: d_sm 4-byte aligned and readable up to
  * sm_off[n] + PV_BLOB_SLACK (records themselves need no alignment), d_pk 16-byte aligned,
@@ -356,7 +389,12 @@ int pv_comm_init(int nranks, int rank, const uint8_t id[128]);
 int pv_allgather_verdicts(const uint64_t* d_local, uint64_t words_per_rank, uint64_t* d_all, void* stream);
 void pv_comm_destroy(void);
 
-/* Device memory helpers so hosts without a GPU framework can stage data (bench, smoke). */
+/* Device memory helpers so hosts without a GPU framework can stage data (bench, smoke).
+ * pv_memcpy_h2d / pv_memcpy_d2h are ordered after every launch enqueued before them (on any stream:
+ * the copy runs on the library stream after the last launch's completion event) and return once the
+ * copy is done. So pv_verify_batch_device(..., NULL) followed by pv_memcpy_d2h of its verdict words
+ * needs no pv_sync, and pv_memcpy_h2d right after a launch never overwrites inputs that launch still
+ * reads. pv_sync waits for all work on the calling thread's current device. */
 int pv_dev_alloc(void** p, uint64_t bytes);
 int pv_dev_free(void* p);
 int pv_memcpy_h2d(void* dst, const void* src, uint64_t bytes);

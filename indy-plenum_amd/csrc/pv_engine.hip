@@ -2020,10 +2020,38 @@ struct Ctx {
         hipEvent_t ev_async = nullptr;
         bool async_pending = false;
     } kc;
+    // zero-copy verdict bytes (pinned, coherent: the host reads them while the kernel runs)
+    uint8_t* h_zc_verdict = nullptr;
+    bool last_zero_copy = false;  // the most recent pv_verify_batch took the zero-copy form
+    // pv_verify_batch_multi_gpu: this device's gathered verdict words (device) and their host copy
+    uint64_t* d_mg = nullptr;
+    uint64_t d_mg_words = 0;
+    uint64_t* h_mg = nullptr;
+    uint64_t h_mg_words = 0;
 };
 
-Ctx g_ctx;
-std::mutex g_mu;
+// One context per device. The single-device ABI (pv_init, pv_verify_batch, ...) works on the device
+// pv_init bound (the primary); pv_init_devices adds contexts for more devices of the same process,
+// which pv_verify_batch_multi_gpu drives from one worker thread per device. g_ctx / g_mu name the
+// calling thread's context: a multi-GPU worker's device (t_dev), else the primary.
+constexpr int PV_MAX_DEV = 16;
+Ctx g_ctxs[PV_MAX_DEV];
+std::mutex g_mus[PV_MAX_DEV];
+std::atomic<int> g_primary{-1};
+thread_local int t_dev = -1;
+inline int pv_cur_dev() {
+    if (t_dev >= 0) return t_dev;
+    const int p = g_primary.load(std::memory_order_acquire);
+    return p >= 0 ? p : 0;
+}
+#define g_ctx (g_ctxs[pv_cur_dev()])
+#define g_mu (g_mus[pv_cur_dev()])
+// Makes `dev` the calling thread's context for the scope (multi-GPU workers, per-device init).
+struct DevScope {
+    int prev;
+    explicit DevScope(int dev) : prev(t_dev) { t_dev = dev; }
+    ~DevScope() { t_dev = prev; }
+};
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -2098,7 +2126,7 @@ int ensure_stage(uint64_t host_bytes, uint64_t dev_bytes) {
         if (g_ctx.h_stage) (void)hipHostFree(g_ctx.h_stage);
         g_ctx.h_stage = nullptr;
         const uint64_t cap = std::max<uint64_t>(host_bytes, 1 << 20);
-        PV_HIP(hipHostMalloc((void**)&g_ctx.h_stage, cap, hipHostMallocDefault), PV_ERR_ALLOC);
+        PV_HIP(hipHostMalloc((void**)&g_ctx.h_stage, cap, hipHostMallocPortable), PV_ERR_ALLOC);
         g_ctx.h_stage_cap = cap;
     }
     if (dev_bytes > g_ctx.d_stage_cap) {
@@ -2425,14 +2453,21 @@ int pv_device_count(void) {
 
 const char* pv_last_error(void) { return g_err.c_str(); }
 
-int pv_init(int device) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (g_ctx.device == device) return PV_OK;
-    if (g_ctx.device >= 0) return fail(PV_ERR_ARG, "pv_init: already bound to another device");
+}  // extern "C"
+
+namespace {
+int check_device_index(int device, const char* who) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
-        return fail(PV_ERR_NO_DEVICE, "pv_init: no HIP device visible");
-    if (device < 0 || device >= ndev) return fail(PV_ERR_ARG, "pv_init: device index out of range");
+        return fail(PV_ERR_NO_DEVICE, std::string(who) + ": no HIP device visible");
+    if (device < 0 || device >= ndev || device >= PV_MAX_DEV)
+        return fail(PV_ERR_ARG, std::string(who) + ": device index out of range");
+    return PV_OK;
+}
+
+// Builds g_ctxs[device] (caller: g_mus[device] held, DevScope(device) active, context not built yet):
+// streams and events, the fixed-base tables, the workspace. Sets the calling thread's HIP device.
+int ctx_init(int device) {
     PV_HIP(hipSetDevice(device), PV_ERR_NO_DEVICE);
     hipDeviceProp_t prop;
     PV_HIP(hipGetDeviceProperties(&prop, device), PV_ERR_NO_DEVICE);
@@ -2577,14 +2612,20 @@ int pv_init(int device) {
             if (rc != PV_OK) return rc;
         }
     }
+    PV_HIP(hipHostMalloc((void**)&g_ctx.h_zc_verdict, PV_ZC_MAX_REQ, hipHostMallocCoherent | hipHostMallocPortable),
+           PV_ERR_ALLOC);
     g_ctx.device = device;
     return PV_OK;
 }
 
-void pv_shutdown(void) {
-    std::lock_guard<std::mutex> lk(g_mu);
+// Frees g_ctxs[t_dev or primary] (caller holds its mutex).
+void ctx_free() {
     if (g_ctx.device < 0) return;
+    (void)hipSetDevice(g_ctx.device);
     if (g_ctx.comm) ncclCommDestroy(g_ctx.comm);
+    if (g_ctx.h_zc_verdict) (void)hipHostFree(g_ctx.h_zc_verdict);
+    if (g_ctx.d_mg) (void)hipFree(g_ctx.d_mg);
+    if (g_ctx.h_mg) (void)hipHostFree(g_ctx.h_mg);
     kc_free();
     if (g_ctx.h_stage) (void)hipHostFree(g_ctx.h_stage);
     if (g_ctx.d_stage) (void)hipFree(g_ctx.d_stage);
@@ -2624,6 +2665,58 @@ void pv_shutdown(void) {
     g_ctx = Ctx();
 }
 
+// In-process multi-GPU state (pv_init_devices): the devices in mask order and one RCCL communicator
+// per device from ncclCommInitAll (a single-process clique).
+struct MultiGpu {
+    std::vector<int> devs;
+    std::vector<ncclComm_t> comms;
+};
+MultiGpu g_mg;
+std::mutex g_mg_mu;
+
+void mg_destroy_comms() {
+    for (ncclComm_t c : g_mg.comms)
+        if (c) ncclCommDestroy(c);
+    g_mg.comms.clear();
+    g_mg.devs.clear();
+}
+}  // namespace
+
+extern "C" {
+
+int pv_init(int device) {
+    const int p = g_primary.load();
+    if (p == device) {
+        PV_HIP(hipSetDevice(device), PV_ERR_NO_DEVICE);  // this thread's device as well
+        return PV_OK;
+    }
+    if (p >= 0) return fail(PV_ERR_ARG, "pv_init: already bound to another device");
+    int rc = check_device_index(device, "pv_init");
+    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_mus[device]);
+        DevScope ds(device);
+        if (g_ctx.device != device && (rc = ctx_init(device)) != PV_OK) return rc;
+    }
+    PV_HIP(hipSetDevice(device), PV_ERR_NO_DEVICE);
+    g_primary.store(device);
+    return PV_OK;
+}
+
+void pv_shutdown(void) {
+    {
+        std::lock_guard<std::mutex> lk(g_mg_mu);
+        mg_destroy_comms();
+    }
+    for (int d = 0; d < PV_MAX_DEV; d++) {
+        std::lock_guard<std::mutex> lk(g_mus[d]);
+        DevScope ds(d);
+        ctx_free();
+    }
+    const int p = g_primary.exchange(-1);
+    if (p >= 0) (void)hipSetDevice(p);
+}
+
 int pv_last_path(int* path, uint32_t* nkeys) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_last_path: call pv_init first");
@@ -2654,8 +2747,10 @@ int pv_last_split(uint32_t* keys, uint32_t* comb_keys, uint32_t* comb_requests) 
 int pv_set_path(int mode) {
     if (mode != PV_PATH_AUTO && mode != PV_PATH_STRAUS && mode != PV_PATH_COMB && mode != PV_PATH_LATENCY)
         return fail(PV_ERR_ARG, "pv_set_path: unknown mode");
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_ctx.path = mode;
+    for (int d = 0; d < PV_MAX_DEV; d++) {  // every device context of the process
+        std::lock_guard<std::mutex> lk(g_mus[d]);
+        g_ctxs[d].path = mode;
+    }
     return PV_OK;
 }
 
@@ -2706,11 +2801,17 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
 
 // Host-side copy pool for the host-buffer entry: persistent threads (created on first use, at most 8,
 // half the host's hardware threads), so a call pays no thread creation. run(k, fn) executes fn(0..k-1)
-// on the pool and the calling thread and returns when all are done. Used under g_mu only.
+// on the pool and the calling thread and returns when all are done. Calls from several threads (the
+// per-device workers of pv_verify_batch_multi_gpu, contexts of different devices) take turns.
 class CopyPool {
    public:
     void run(unsigned k, const std::function<void(unsigned)>& fn) {
-        if (k <= 1 || workers() == 0) {
+        if (k <= 1) {
+            for (unsigned i = 0; i < k; i++) fn(i);
+            return;
+        }
+        std::lock_guard<std::mutex> turn(run_mu_);
+        if (workers() == 0) {
             for (unsigned i = 0; i < k; i++) fn(i);
             return;
         }
@@ -2765,7 +2866,7 @@ class CopyPool {
             drain();
         }
     }
-    std::mutex m_;
+    std::mutex m_, run_mu_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(unsigned)>* fn_ = nullptr;
     unsigned next_ = 0, total_ = 0, done_ = 0;
@@ -2807,6 +2908,8 @@ static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* s
 #endif
 static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async);
 static void kc_auto_count(const uint8_t* pk, uint64_t n, std::vector<uint8_t>& admit);
+static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk, uint64_t* d_out,
+                            uint64_t** dver_out, uint64_t** hver_out);
 
 static bool pv_keyed_hint(const uint8_t* pk, uint64_t n) {
     if (g_ctx.path != PV_PATH_AUTO || n < PV_KEYED_HINT_MIN || n > PV_LATENCY_MAX) return false;
@@ -2853,11 +2956,10 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
         if (!g_ctx.timing && n <= PV_ZC_MAX_REQ && stride <= PV_ZC_MAX_STRIDE &&
             (g_ctx.path == PV_PATH_LATENCY ||
              (g_ctx.path == PV_PATH_AUTO && n <= PV_LATENCY_MAX && !pv_keyed_hint(pk, n)))) {
-            const uint64_t vbytes = PV_ZC_MAX_REQ;
-            int rc = ensure_stage(vbytes + n * stride, 0);
+            int rc = ensure_stage(n * stride, 0);
             if (rc) return rc;
-            uint8_t* vb = g_ctx.h_stage;
-            uint8_t* slots = g_ctx.h_stage + vbytes;
+            uint8_t* vb = g_ctx.h_zc_verdict;  // coherent pinned memory, read while the kernel runs
+            uint8_t* slots = g_ctx.h_stage;
             memset(vb, 0xFF, n);  // pending (PV_ZC_SPIN)
             auto fill = [&](uint64_t a, uint64_t b) {
                 for (uint64_t i = a; i < b; i++) {
@@ -2882,6 +2984,7 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
             g_ctx.last_latency = true;
             g_ctx.last_keyed = false;
             g_ctx.last_dev_choice = false;
+            g_ctx.last_zero_copy = true;
             rc = pv_latency_launch_zc(slots, (uint32_t)stride, n, g_ctx.d_bcomb, kc_view(), vb, s);
             PV_HIP(hipEventRecord(g_ctx.ev_launch_done, s), PV_ERR_LAUNCH);
             g_ctx.last_stream = s;
@@ -2897,6 +3000,24 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
         }
     }
 #endif
+    uint64_t *dver = nullptr, *hver = nullptr;
+    int rc = stage_and_launch(sm, sm_off, n, pk, nullptr, &dver, &hver);
+    if (rc) return rc;
+    PV_HIP(hipMemcpyAsync(hver, dver, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, g_ctx.stream), PV_ERR_LAUNCH);
+    rc = kc_auto_after_batch(pk, n, g_ctx.stream);
+    if (rc) return rc;
+    memcpy(verdict_bits, hver, (n + 7) / 8);  // little-endian words, LSB-first bits
+    return PV_OK;
+}
+
+// The copy form of a host-buffer batch on the calling thread's context: stages the keys, offsets and
+// records into the pinned / device staging areas (pipelined with the H2D DMA for large blobs) and
+// enqueues the verification on the context's stream. d_out: where the verdict words go (nullptr =
+// the staging area's own verdict section); *dver / *hver receive the staging area's device / pinned
+// verdict sections.
+static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk, uint64_t* d_out,
+                            uint64_t** dver_out, uint64_t** hver_out) {
+    g_ctx.last_zero_copy = false;
     // staging layout (one pinned buffer, one device buffer, 256-B aligned sections):
     //   [pk n*32][off (n+1) u64][verdict ceil(n/64) u64][blob + PV_BLOB_SLACK]
     auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
@@ -2944,19 +3065,17 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
         }
     }
     uint64_t* dver = reinterpret_cast<uint64_t*>(d + pk_bytes + off_bytes);
-    g_ctx.verdict_zeroed = true;
+    g_ctx.verdict_zeroed = d_out == nullptr;
     g_ctx.keyed_hint = pv_keyed_hint(pk, n);
     g_ctx.hint_set = true;
-    rc = launch(d + pk_bytes + off_bytes + v_bytes, reinterpret_cast<const uint64_t*>(d + pk_bytes), n, d, dver, s);
+    rc = launch(d + pk_bytes + off_bytes + v_bytes, reinterpret_cast<const uint64_t*>(d + pk_bytes), n, d,
+                d_out ? d_out : dver, s);
     g_ctx.verdict_zeroed = false;
     g_ctx.keyed_hint = false;
     g_ctx.hint_set = false;
     if (rc) return rc;
-    uint64_t* hver = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
-    PV_HIP(hipMemcpyAsync(hver, dver, vwords * 8, hipMemcpyDeviceToHost, s), PV_ERR_LAUNCH);
-    rc = kc_auto_after_batch(pk, n, s);
-    if (rc) return rc;
-    memcpy(verdict_bits, hver, (n + 7) / 8);  // little-endian words, LSB-first bits
+    *dver_out = dver;
+    *hver_out = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
     return PV_OK;
 }
 
@@ -3044,6 +3163,160 @@ void pv_comm_destroy(void) {
     g_ctx.comm = nullptr;
 }
 
+int pv_shard_plan(uint64_t n, int ndev, uint64_t* bounds, uint64_t* words_per_shard) {
+    if (ndev < 1 || ndev > PV_MAX_DEV || !bounds || !words_per_shard) return fail(PV_ERR_ARG, "pv_shard_plan: bad arguments");
+    // whole 64-request verdict words per shard (sharding.py shard_bounds): word ranges
+    // [words r / G, words (r + 1) / G), so every shard but the last is a multiple of 64 requests
+    const uint64_t words = (n + 63) / 64;
+    uint64_t wmax = 0;
+    for (int r = 0; r <= ndev; r++) bounds[r] = std::min<uint64_t>(n, 64 * (words * (uint64_t)r / (uint64_t)ndev));
+    for (int r = 0; r < ndev; r++)
+        wmax = std::max<uint64_t>(wmax, words * (uint64_t)(r + 1) / ndev - words * (uint64_t)r / ndev);
+    *words_per_shard = wmax;
+    return PV_OK;
+}
+
+int pv_init_devices(uint32_t device_mask) {
+    std::vector<int> devs;
+    for (int d = 0; d < PV_MAX_DEV; d++)
+        if ((device_mask >> d) & 1u) devs.push_back(d);
+    if (devs.empty() || (device_mask >> PV_MAX_DEV) != 0) return fail(PV_ERR_ARG, "pv_init_devices: bad device mask");
+    for (int d : devs) {
+        const int rc = check_device_index(d, "pv_init_devices");
+        if (rc) return rc;
+    }
+    std::lock_guard<std::mutex> mg(g_mg_mu);
+    // the missing contexts are built in parallel, one host thread per device (tables built on each GPU)
+    std::vector<int> rcs(devs.size(), PV_OK);
+    std::vector<std::string> errs(devs.size());
+    {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < devs.size(); i++)
+            th.emplace_back([&, i] {
+                const int d = devs[i];
+                std::lock_guard<std::mutex> lk(g_mus[d]);
+                DevScope ds(d);
+                if (g_ctx.device != d && (rcs[i] = ctx_init(d)) != PV_OK) errs[i] = g_err;
+            });
+        for (auto& t : th) t.join();
+    }
+    for (size_t i = 0; i < devs.size(); i++)
+        if (rcs[i]) return fail(rcs[i], "pv_init_devices: device " + std::to_string(devs[i]) + ": " + errs[i]);
+    if (g_mg.devs != devs) {
+        mg_destroy_comms();
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        std::vector<ncclComm_t> comms(devs.size(), nullptr);
+        const ncclResult_t r = ncclCommInitAll(comms.data(), (int)devs.size(), devs.data());
+        (void)hipSetDevice(cur);  // the caller's current device is unchanged
+        if (r != ncclSuccess) return fail(PV_ERR_COMM, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+        g_mg.comms = comms;
+        g_mg.devs = devs;
+    }
+    return PV_OK;
+}
+
+int pv_multi_gpu_devices(int* devices, int max_devices) {
+    std::lock_guard<std::mutex> mg(g_mg_mu);
+    for (int i = 0; i < (int)g_mg.devs.size() && i < max_devices && devices; i++) devices[i] = g_mg.devs[i];
+    return (int)g_mg.devs.size();
+}
+
+int pv_verify_batch_multi_gpu(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
+                              uint8_t* verdict_bits) {
+    if (n == 0) return PV_OK;
+    if (!sm || !sm_off || !pk || !verdict_bits) return fail(PV_ERR_ARG, "null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if (sm_off[i + 1] < sm_off[i]) return fail(PV_ERR_ARG, "sm_off must be non-decreasing");
+    std::lock_guard<std::mutex> mg(g_mg_mu);
+    const int G = (int)g_mg.devs.size();
+    if (G == 0) return fail(PV_ERR_NOT_INIT, "pv_verify_batch_multi_gpu: call pv_init_devices first");
+    std::vector<uint64_t> b(G + 1);
+    uint64_t wpr = 0;
+    int rc = pv_shard_plan(n, G, b.data(), &wpr);
+    if (rc) return rc;
+    // every device's context for the whole call (ascending device order: no lock-order inversion)
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (int d : g_mg.devs) locks.emplace_back(g_mus[d]);
+    // one worker per device: stage its shard (host -> pinned -> HBM, its own stream) and enqueue the
+    // shard's verification with the verdict words landing in its slot of the gather buffer
+    std::vector<int> rcs(G, PV_OK);
+    std::vector<std::string> errs(G);
+    {
+        std::vector<std::thread> th;
+        for (int r = 0; r < G; r++)
+            th.emplace_back([&, r] {
+                const int d = g_mg.devs[r];
+                DevScope ds(d);
+                auto run = [&]() -> int {
+                    PV_HIP(hipSetDevice(d), PV_ERR_NO_DEVICE);
+                    Ctx& c = g_ctx;
+                    const uint64_t need = (uint64_t)G * wpr;
+                    if (c.d_mg_words < need) {
+                        if (c.d_mg) (void)hipFree(c.d_mg);
+                        c.d_mg = nullptr;
+                        c.d_mg_words = 0;
+                        PV_HIP(hipMalloc((void**)&c.d_mg, need * 8), PV_ERR_ALLOC);
+                        c.d_mg_words = need;
+                    }
+                    if (c.last_stream && c.last_stream != c.stream)
+                        PV_HIP(hipStreamWaitEvent(c.stream, c.ev_launch_done, 0), PV_ERR_LAUNCH);
+                    PV_HIP(hipMemsetAsync(c.d_mg + (uint64_t)r * wpr, 0, wpr * 8, c.stream), PV_ERR_LAUNCH);
+                    const uint64_t lo = b[r], hi = b[r + 1];
+                    if (hi == lo) return PV_OK;
+                    uint64_t *dv = nullptr, *hv = nullptr;
+                    return stage_and_launch(sm, sm_off + lo, hi - lo, pk + 32 * lo, c.d_mg + (uint64_t)r * wpr, &dv, &hv);
+                };
+                if ((rcs[r] = run()) != PV_OK) errs[r] = g_err;
+            });
+        for (auto& t : th) t.join();
+    }
+    for (int r = 0; r < G; r++)
+        if (rcs[r]) {
+            for (int d : g_mg.devs) (void)hipStreamSynchronize(g_ctxs[d].stream);  // no DMA still reads staging
+            return fail(rcs[r], "pv_verify_batch_multi_gpu: device " + std::to_string(g_mg.devs[r]) + ": " + errs[r]);
+        }
+    // ONE all-gather of the per-shard verdict words over the devices' RCCL clique (in place: shard r
+    // sits at r * wpr on every device), then the gathered words come back from the first device
+    ncclResult_t nr = ncclGroupStart();
+    for (int r = 0; r < G && nr == ncclSuccess; r++) {
+        Ctx& c = g_ctxs[g_mg.devs[r]];
+        nr = ncclAllGather(c.d_mg + (uint64_t)r * wpr, c.d_mg, wpr, ncclUint64, g_mg.comms[r], c.stream);
+    }
+    const ncclResult_t ne = ncclGroupEnd();
+    if (nr == ncclSuccess) nr = ne;
+    Ctx& c0 = g_ctxs[g_mg.devs[0]];
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    rc = PV_OK;
+    if (nr != ncclSuccess) rc = fail(PV_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+    if (rc == PV_OK && c0.h_mg_words < (uint64_t)G * wpr) {
+        if (c0.h_mg) (void)hipHostFree(c0.h_mg);
+        c0.h_mg = nullptr;
+        c0.h_mg_words = 0;
+        if (hipSetDevice(c0.device) != hipSuccess ||
+            hipHostMalloc((void**)&c0.h_mg, (uint64_t)G * wpr * 8, hipHostMallocPortable) != hipSuccess)
+            rc = fail(PV_ERR_ALLOC, "pv_verify_batch_multi_gpu: pinned verdict buffer");
+        else
+            c0.h_mg_words = (uint64_t)G * wpr;
+    }
+    if (rc == PV_OK && hipMemcpyAsync(c0.h_mg, c0.d_mg, (uint64_t)G * wpr * 8, hipMemcpyDeviceToHost, c0.stream) != hipSuccess)
+        rc = fail(PV_ERR_LAUNCH, "pv_verify_batch_multi_gpu: verdict copy");
+    for (int r = 0; r < G; r++) {
+        Ctx& c = g_ctxs[g_mg.devs[r]];
+        const hipError_t e = hipStreamSynchronize(c.stream);
+        if (e != hipSuccess && rc == PV_OK)
+            rc = fail(PV_ERR_LAUNCH, std::string("pv_verify_batch_multi_gpu: ") + hipGetErrorString(e));
+    }
+    (void)hipSetDevice(cur);
+    if (rc) return rc;
+    for (int r = 0; r < G; r++) {  // shard r's words start at bit b[r] (a multiple of 64)
+        const uint64_t lo = b[r], hi = b[r + 1];
+        if (hi > lo) memcpy(verdict_bits + lo / 8, c0.h_mg + (uint64_t)r * wpr, (hi - lo + 7) / 8);
+    }
+    return PV_OK;
+}
+
 int pv_dev_alloc(void** p, uint64_t bytes) {
     PV_HIP(hipMalloc(p, std::max<uint64_t>(bytes, 16)), PV_ERR_ALLOC);
     return PV_OK;
@@ -3052,13 +3325,35 @@ int pv_dev_free(void* p) {
     PV_HIP(hipFree(p), PV_ERR_ALLOC);
     return PV_OK;
 }
-int pv_memcpy_h2d(void* dst, const void* src, uint64_t bytes) {
-    PV_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), PV_ERR_LAUNCH);
+}  // extern "C"
+
+namespace {
+// A copy ordered after every launch enqueued so far on the primary context, whatever stream the caller
+// gave it: the library stream first waits for the last launch's completion event, then copies; the
+// call returns once the copy is done. (A plain null-stream hipMemcpy is not ordered after the
+// library's non-blocking streams: a D2H could read verdict words before the launch wrote them, an H2D
+// could overwrite inputs a running launch still reads.)
+int ordered_copy(void* dst, const void* src, uint64_t bytes, hipMemcpyKind kind) {
+    if (bytes == 0) return PV_OK;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ctx.device < 0) {
+        PV_HIP(hipMemcpy(dst, src, bytes, kind), PV_ERR_LAUNCH);
+        return PV_OK;
+    }
+    hipStream_t s = g_ctx.stream;
+    if (g_ctx.last_stream && g_ctx.last_stream != s) PV_HIP(hipStreamWaitEvent(s, g_ctx.ev_launch_done, 0), PV_ERR_LAUNCH);
+    PV_HIP(hipMemcpyAsync(dst, src, bytes, kind, s), PV_ERR_LAUNCH);
+    PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
     return PV_OK;
 }
-int pv_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
-    PV_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
-    return PV_OK;
+}  // namespace
+
+extern "C" {
+int pv_memcpy_h2d(void* dst, const void* src, uint64_t bytes) { return ordered_copy(dst, src, bytes, hipMemcpyHostToDevice); }
+int pv_memcpy_d2h(void* dst, const void* src, uint64_t bytes) { return ordered_copy(dst, src, bytes, hipMemcpyDeviceToHost); }
+int pv_last_zero_copy(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_ctx.last_zero_copy ? 1 : 0;
 }
 int pv_sync(void) {
     PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);

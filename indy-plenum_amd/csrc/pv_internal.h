@@ -26,7 +26,10 @@ int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, co
 // per request to h_vbytes (pinned host memory).
 int pv_latency_launch_zc(const uint8_t* h_slots, uint32_t stride, uint64_t n, const void* d_bcomb,
                          const PvKeyCacheView& kc, uint8_t* h_vbytes, hipStream_t stream);
-static constexpr uint64_t PV_ZC_MAX_REQ = 2048;     // = PV_LATENCY_MAX (four-wave form up to PV_LAT4_MAX)
+// the largest zero-copy call: the latency range AUTO uses for host buffers without a key-repeat hint
+// (PV_KEYED_HINT_MIN - 1 = 2,048; PV_LATENCY_MAX, 4,096, bounds the device-side choice). The four-wave
+// form runs up to PV_LAT4_MAX, the two-wave form above it
+static constexpr uint64_t PV_ZC_MAX_REQ = 2048;
 static constexpr uint32_t PV_ZC_MAX_STRIDE = 2048;  // bytes per slot (the LDS copy)
 static constexpr uint32_t PV_ZC_PK_WORD = 4, PV_ZC_REC_WORD = 12, PV_ZC_SLACK = 160;
 

@@ -76,6 +76,12 @@ SIGNATURES = {
     "pv_key_cache_contains": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_key_cache_auto": (ctypes.c_int, [ctypes.c_uint32]),
     "pv_key_cache_auto_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "pv_last_zero_copy": (ctypes.c_int, []),
+    "pv_init_devices": (ctypes.c_int, [ctypes.c_uint32]),
+    "pv_verify_batch_multi_gpu": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                 ctypes.c_void_p]),
+    "pv_multi_gpu_devices": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "pv_shard_plan": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, _c_u64p, _c_u64p]),
     "pv_stream_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "pv_stream_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_stream_sync": (ctypes.c_int, [ctypes.c_void_p]),
@@ -162,6 +168,80 @@ def verify_sm_batch(blob, offsets, pks):
     bits = np.zeros((n + 7) // 8, dtype=np.uint8)
     check(L.pv_verify_batch(_ptr(blob), _ptr(offsets), n, _ptr(pks), _ptr(bits)), "pv_verify_batch")
     return np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+
+
+def last_zero_copy():
+    """True if the most recent host-buffer call (pv_verify_batch) took the zero-copy form."""
+    return bool(lib().pv_last_zero_copy())
+
+
+def shard_plan(n, ndev):
+    """(bounds uint64[ndev + 1], verdict words per shard) of pv_verify_batch_multi_gpu's split of n
+    requests over ndev devices (host-only, no GPU needed)."""
+    b = np.zeros(ndev + 1, np.uint64)
+    w = ctypes.c_uint64()
+    check(lib().pv_shard_plan(int(n), int(ndev), b.ctypes.data_as(_c_u64p), ctypes.byref(w)), "pv_shard_plan")
+    return b, w.value
+
+
+_multi_devices = None
+
+
+def ensure_devices(devices):
+    """Bind this process to several GPUs for pv_verify_batch_multi_gpu (one context and one RCCL
+    communicator per device, ncclCommInitAll). Raises NativeUnavailable when they are not visible."""
+    global _multi_devices
+    devices = tuple(sorted(set(int(d) for d in devices)))
+    if _multi_devices == devices:
+        return devices
+    L = lib()
+    ndev = L.pv_device_count()
+    if ndev <= 0:
+        raise NativeUnavailable("no HIP device visible: the verification engine is GPU-only")
+    if not devices or devices[-1] >= ndev or devices[0] < 0:
+        raise NativeUnavailable("devices %s not visible (%d GPUs)" % (list(devices), ndev))
+    mask = 0
+    for d in devices:
+        mask |= 1 << d
+    rc = L.pv_init_devices(mask)
+    if rc != PV_OK:
+        raise NativeUnavailable("pv_init_devices failed: %s" % L.pv_last_error().decode(errors="replace"))
+    _multi_devices = devices
+    return devices
+
+
+def verify_sm_batch_multi(blob, offsets, pks, devices=None):
+    """verify_sm_batch sharded over several GPUs of this process (pv_verify_batch_multi_gpu: one shard
+    per device, verdict bitmaps gathered with one RCCL all-gather). devices: the GPUs to use (default:
+    every visible one, or the set already bound)."""
+    if devices is None:
+        devices = _multi_devices or range(max(1, lib().pv_device_count()))
+    ensure_devices(devices)
+    L = lib()
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    if n <= 0:
+        return np.zeros(0, dtype=bool)
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    if blob.size == 0:
+        blob = np.zeros(1, dtype=np.uint8)
+    pks = np.ascontiguousarray(pks, dtype=np.uint8).reshape(n, 32)
+    bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+    check(L.pv_verify_batch_multi_gpu(_ptr(blob), _ptr(offsets), n, _ptr(pks), _ptr(bits)),
+          "pv_verify_batch_multi_gpu")
+    return np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+
+
+def multi_gpu_engine(devices):
+    """An engine callable (blob, off, pks) -> verdicts for authenticate_batch(engine=...) that shards
+    every batch over `devices` (SURVEY.md §8b pv_verify_batch_multi_gpu)."""
+    devices = tuple(devices)
+
+    def engine(blob, off, pks):
+        return verify_sm_batch_multi(blob, off, pks, devices)
+
+    engine.devices = devices
+    return engine
 
 
 def set_path(mode):

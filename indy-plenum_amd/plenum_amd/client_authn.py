@@ -297,9 +297,13 @@ class CoreAuthMixin:
         return pairs
 
     def authenticate_batch(self, reqs, threshold: Optional[int] = None, verifier: Verifier = DidVerifier,
-                           engine=None):
+                           engine=None, devices=None):
         """authenticate() for every request in ``reqs`` with all signature checks in one GPU launch.
-        Returns, per request, what authenticate() returns or the exception instance it raises."""
+        Returns, per request, what authenticate() returns or the exception instance it raises.
+        ``devices``: shard the checks over those GPUs of this process (pv_verify_batch_multi_gpu)."""
+        if engine is None and devices is not None:
+            from . import _native
+            engine = _native.multi_gpu_engine(devices)
         cache = batch.VerdictCache()
         cache.fill(self.plan_verifications(reqs, verifier), engine)
         results = []

@@ -68,9 +68,14 @@ class ReqAuthenticator:
     def clean_from_verified(self, key):
         self._verified_reqs.pop(key, None)
 
-    def authenticate_batch(self, items, engine=None):
+    def authenticate_batch(self, items, engine=None, devices=None):
         """[(req_data, key)] -> per item: the identifier set authenticate() returns, or the
-        exception instance it raises."""
+        exception instance it raises. ``devices`` (a list of GPU indices): shard the batch's
+        signature checks over those GPUs of this process (pv_verify_batch_multi_gpu), unless an
+        ``engine`` is given."""
+        if engine is None and devices is not None:
+            from . import _native
+            engine = _native.multi_gpu_engine(devices)
         per_authnr = {}
         for req_data, key in items:
             if key and self._check_and_verify_existing_req(req_data, key):

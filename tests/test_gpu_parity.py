@@ -106,18 +106,27 @@ def test_repeated_keys_with_adversarial(native, sodium, oracle):
     assert 0.85 * len(cases) < want.sum() < len(cases)
 
 
-def test_small_calls_long_records(native, sodium, oracle):
-    """Small host-buffer calls (the latency path's zero-copy form in AUTO / LATENCY: the kernel reads the
-    pinned staging buffer and copies each record into LDS when it fits, else reads it in place) with
-    records around and beyond the LDS copy's size, valid and tampered, at every alignment."""
-    g = VectorGen(sodium, oracle, seed=16)
+def _long_record_cases(sodium, oracle, lengths, seed):
+    g = VectorGen(sodium, oracle, seed=seed)
     cases = []
-    for ln in list(range(1700, 1960, 20)) + [0, 1, 127, 128, 4000, 9000]:
+    for ln in lengths:
         sm, pk = g.valid(bytes(g.rng.getrandbits(8) for _ in range(ln)))
         cases.append((sm, pk))
         bad = bytearray(sm)
         bad[-1 if ln else 0] ^= 0x10
         cases.append((bytes(bad), pk))
+    return cases
+
+
+def test_small_calls_zero_copy_records(native, sodium, oracle):
+    """Small host-buffer calls whose records all fit a zero-copy slot (sm <= 1,840 bytes: the slot's
+    2,048-byte stride holds the 48-byte header, the record and the hash's 160-byte read-ahead, which
+    ends exactly at the slot's edge for the longest records): on the latency path the call IS
+    zero-copy (the kernel reads the pinned slots over PCIe and copies each record into LDS), valid
+    and tampered records, every alignment. pv_last_zero_copy says which form ran."""
+    lengths = list(range(1700, 1777, 4)) + [1776, 0, 1, 127, 128]
+    cases = _long_record_cases(sodium, oracle, lengths, seed=16)
+    assert max(len(sm) for sm, _ in cases) == 1840
     blob, off, pks = pack(cases)
     want = reference_verdicts(sodium, cases)
     assert want.sum() == len(cases) // 2
@@ -125,3 +134,20 @@ def test_small_calls_long_records(native, sodium, oracle):
         blob2 = np.concatenate([np.full(lead, 0x55, np.uint8), blob])
         got = native.verify_sm_batch(blob2, off + lead, pks)
         assert np.array_equal(got, want), (lead, np.nonzero(got != want)[0][:8])
+        assert native.last_zero_copy() == (native.last_path()[0] == native.PV_PATH_LATENCY), lead
+
+
+def test_small_calls_long_records(native, sodium, oracle):
+    """Small host-buffer calls with records beyond a zero-copy slot (1,841 bytes up to 9 KB): the
+    whole call takes the staged copy form (the zero-copy choice is made per call from the longest
+    record), valid and tampered, at every alignment."""
+    lengths = list(range(1780, 1960, 20)) + [4000, 9000]
+    cases = _long_record_cases(sodium, oracle, lengths, seed=17)
+    blob, off, pks = pack(cases)
+    want = reference_verdicts(sodium, cases)
+    assert want.sum() == len(cases) // 2
+    for lead in (0, 1, 2, 3):
+        blob2 = np.concatenate([np.full(lead, 0x55, np.uint8), blob])
+        got = native.verify_sm_batch(blob2, off + lead, pks)
+        assert np.array_equal(got, want), (lead, np.nonzero(got != want)[0][:8])
+        assert not native.last_zero_copy()
