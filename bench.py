@@ -505,22 +505,24 @@ def workload_name(n, world):
 
 
 def assemble_result(world, n, steps, warmup, elapsed, stage_ms, chunks, comb, nkeys, record_bytes_avg,
-                    ok_local, ok_all, per_gpu_fixed=False):
+                    ok_local, ok_all, per_gpu_fixed=False, fused=False):
     """The headline bench line from the measured quantities (every rank count; the optional legs are
     added by the caller): value = requests of all ranks / the max-over-ranks time of `steps` steps,
     the roofline of the dominant kernel from its HIP-event launch time (stage "msm" / chunks), the
-    whole-pipeline figures from the stage times."""
+    whole-pipeline figures from the stage times. fused: the comb path's MSM stage is pv_comb_ab_kernel
+    ([S]B and [k](-A) in one kernel), else pv_comb_a_kernel ([k](-A) only)."""
     total = n * world * steps
     value = total / elapsed
     ms_per_step = 1e3 * elapsed / steps
-    mac_kernel = BC.MAC_COMB_MSM_KERNEL if comb else BC.MAC_MSM_HALF_KERNEL
+    mac_kernel = ((BC.MAC_COMB_AB_KERNEL if fused else BC.MAC_COMB_MSM_KERNEL) if comb
+                  else BC.MAC_MSM_HALF_KERNEL)
     launch_ms = stage_ms["msm"] / chunks  # the roofline kernel's average launch (one per chunk)
     achieved = mac_kernel * (n / chunks) / (launch_ms * 1e-3)
     pipeline_ms = sum(stage_ms.values())
     per_gpu_rate = n / (pipeline_ms * 1e-3)
     mac_executed = (BC.MAC_COMB_MSM + BC.MAC_ENCODE / 4 + BC.MAC_COMB_PER_KEY * nkeys / (n / chunks)) if comb \
         else (BC.MAC_PER_VERIFY - BC.MAC_ENCODE * 3 / 4)
-    kernel = "pv_comb_a_kernel" if comb else "pv_msm_kernel"
+    kernel = ("pv_comb_ab_kernel" if fused else "pv_comb_a_kernel") if comb else "pv_msm_kernel"
     return {
         "metric": METRIC, "value": round(value, 1), "unit": "verifies/s", "n_gpus": world, "steps": steps,
         "warmup": warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
@@ -849,7 +851,8 @@ def main():
         ok_all = all(np.array_equal(bits(allw[r], n), expected_bits(n, r)) for r in range(world))
 
     result = assemble_result(world, n, args.steps, args.warmup, elapsed, stage_ms, chunks, comb, nkeys,
-                             float(blob.nbytes) / n, ok_local, ok_all, per_gpu_fixed=bool(args.per_gpu))
+                             float(blob.nbytes) / n, ok_local, ok_all, per_gpu_fixed=bool(args.per_gpu),
+                             fused=_native.comb_fused())
     if world > 1 and not args.no_host_path:
         # SURVEY.md §8e host traffic: each rank's shard from host buffers (pv_verify_batch: pinned
         # staging pipelined with the H2D DMA, kernels, verdicts back), on up to configs[4]'s 8M-request

@@ -64,6 +64,9 @@ MAC_COMB_MSM = MAC_PER_MUL * (32 * 8 + 10 * 7 + 2 - 1)
 # pv_comb_a_kernel (the 32 T_A additions, the MSM stage and the roofline kernel)
 MAC_COMB_B_KERNEL = MAC_PER_MUL * (10 * 7 + 2)
 MAC_COMB_MSM_KERNEL = MAC_PER_MUL * (32 * 8 - 1)
+# the fused build (PV_BUILD_COMB_FUSED, round 4): pv_comb_ab_kernel runs both halves, [S]B's 10 niels
+# additions and the 32 T_A additions, so its algorithmic work is the whole per-request comb count
+MAC_COMB_AB_KERNEL = MAC_COMB_MSM
 # per distinct key (amortised over the requests that share it): decompression + 31 x 8 doublings
 # (4 S + 3 M, the last of each 8 to extended: +1 M) + 32 x 129 table entries (8 M + 1 M each)
 MAC_COMB_PER_KEY = _mac(_S_DECOMP, _M_DECOMP) + _mac(31 * 8 * 4, 31 * (8 * 3 + 1)) + MAC_PER_MUL * 32 * 129 * 9

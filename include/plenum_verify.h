@@ -60,6 +60,12 @@ extern "C" {
 /* ABI version of this header. */
 #define PV_ABI_VERSION 1
 int pv_abi_version(void);
+/* Build configuration of the library's kernels (bit set = compiled in):
+ *   PV_BUILD_COMB_FUSED  the keyed comb path computes [S]B and [k](-A) in ONE kernel
+ *                        (pv_comb_ab_kernel, the MSM stage) instead of pv_comb_b_kernel (TABLE stage)
+ *                        + pv_comb_a_kernel (MSM stage) */
+#define PV_BUILD_COMB_FUSED 1u
+uint32_t pv_build_flags(void);
 
 /* Number of visible GPUs (0 when none; never an error). */
 int pv_device_count(void);

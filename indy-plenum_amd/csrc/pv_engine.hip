@@ -72,6 +72,12 @@ static constexpr int PV_BLOCK = 256;
 #ifndef PV_PREP_MINBLOCKS
 #define PV_PREP_MINBLOCKS 2  // Straus prep (decompression + SHA-512 + recoding)
 #endif
+// Dynamic LDS requested by every pv_comb_prep_kernel workgroup, unused: it caps the kernel's residency
+// so that the key chain, launched beside it on the key stream, finds a wave slot on every SIMD at
+// once instead of waiting for prep workgroups to retire (env PV_PREP_LDS_PAD overrides at pv_init).
+#ifndef PV_PREP_LDS_PAD
+#define PV_PREP_LDS_PAD 0
+#endif
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
 // AUTO: chunks above the latency path's range go keyed (dedup, then comb keys / Straus side). At
@@ -332,6 +338,7 @@ struct Work {
     uint32_t* q;
     uint4* qb;        // [S]B per REQUEST of a keyed chunk, 160 B each (pv_comb_b_req_kernel)
     uint64_t stride;  // chunk capacity (requests)
+    uint4* aos;       // per REQUEST comb-prep results, PrepAos<W>::Q uint4 each (pv_comb_prep_req_kernel)
 };
 
 // How a chunk's requests are split between the two arithmetic paths, decided ON THE DEVICE by the
@@ -1619,6 +1626,95 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_kernel(const uint8_t
     }
 }
 
+// Request-order form of the comb prep (PV_PREP_REQ_ORDER). Slot order gives every lane a record at a
+// random place in the blob, and a record's 128-byte SHA-512 blocks straddle cache lines that the next
+// block re-reads long after they left L2 (round 3 PMC: 1.06 GB fetched per 1M launch for ~0.42 GB of
+// records and keys). In request order the 64 lanes of a wave read 64 CONSECUTIVE records, ~23 KB of
+// contiguous blob, so the lines that straddle two lanes' records or two blocks of one record are
+// reused within the wave's own burst. The per-request results (radix-256 digits of k, radix-2^W digits
+// of S, the signature-check flag) go to a per-request AoS record, written coalesced;
+// pv_comb_digits_kernel then gathers them into the slot-ordered rows the comb kernel reads.
+#ifndef PV_PREP_REQ_ORDER
+#define PV_PREP_REQ_ORDER 1
+#endif
+template <int W>
+struct PrepAos {  // uint4 per request: ek[8], fb[POS], flag, padding
+    static constexpr int WORDS = 8 + Bc2<W>::POS + 1;
+    static constexpr int Q = (WORDS + 3) / 4;
+};
+static constexpr int PV_PREP_AOS_QMAX = 7;  // the largest PrepAos<W>::Q (W = 16: 25 words)
+static_assert(PrepAos<16>::Q <= PV_PREP_AOS_QMAX && PrepAos<PV_BC2_W>::Q <= PV_PREP_AOS_QMAX, "AoS record size");
+template <int W>
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_prep_req_kernel(const uint8_t* __restrict__ sm,
+                                                                        const uint64_t* __restrict__ off, uint64_t n,
+                                                                        const uint8_t* __restrict__ pk, Work wk,
+                                                                        KeyWork kw, Gate gate) {
+    if (!gate.keyed() || gate.off()) return;
+    const uint32_t r = blockIdx.x * PV_BLOCK + threadIdx.x;  // request
+    if (r >= n) return;
+    const uint32_t i = kw.req_pos[r];  // its slot
+    if (i >= gate.ncomb()) return;     // a Straus-path request (its prep runs on the side stream)
+    const uint64_t o0 = off[r], o1 = off[r + 1];
+    const uint64_t smlen = o1 - o0;
+    const uint64_t raddr = reinterpret_cast<uint64_t>(sm + o0);
+    const DevMsg mw{reinterpret_cast<const uint32_t*>(raddr & ~3ull), (uint32_t)(raddr & 3)};
+    pv_sig_words in;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        in.R[q] = mw.dw(q);
+        in.S[q] = mw.dw(8 + q);
+    }
+    pv_load_pk(in.A, pk, r);
+    const bool ok = pv_sig_ok(in, smlen);
+    uint32_t k[8];
+    pv_hash_k(k, in, smlen, mw);
+    constexpr int P = Bc2<W>::POS;
+    uint32_t w[4 * PrepAos<W>::Q];
+    sc_recode256(w, k);
+    int32_t fb[P];
+    sc_recode_w<W, P>(fb, in.S);
+#pragma unroll
+    for (int j = 0; j < P; j++) w[8 + j] = (uint32_t)fb[j];
+    w[8 + P] = ok ? 1u : 0u;
+#pragma unroll
+    for (int j = 9 + P; j < 4 * PrepAos<W>::Q; j++) w[j] = 0u;
+    uint4* o = wk.aos + (uint64_t)r * PrepAos<W>::Q;
+#pragma unroll
+    for (int q = 0; q < PrepAos<W>::Q; q++) o[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    if (kw.nkeys[PV_SPLIT_SPARSE]) {  // small chunk: record which entries of each row this request uses
+        uint32_t* nd = kw.need + (uint64_t)kw.skey[i] * PV_COMB_POS * 5;
+#pragma unroll
+        for (int pos = 0; pos < PV_COMB_POS; pos++) {
+            const int e = pv_byte(w[pos >> 2], pos);
+            const uint32_t d = (uint32_t)(e < 0 ? -e : e);
+            atomicOr(nd + pos * 5 + (d >> 5), 1u << (d & 31));
+        }
+    }
+}
+
+// Slot order: every comb slot's digit rows and flag from its request's AoS record (80-112 contiguous
+// bytes per lane), written as the coalesced rows pv_comb_ab_kernel / pv_comb_a_kernel and the encode read.
+template <int W>
+__global__ __launch_bounds__(PV_BLOCK) void pv_comb_digits_kernel(Work wk, KeyWork kw, Gate gate) {
+    if (!gate.keyed() || gate.off()) return;
+    const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
+    if (i >= gate.ncomb()) return;
+    const uint4* a = wk.aos + (uint64_t)kw.slot_req[i] * PrepAos<W>::Q;
+    uint32_t w[4 * PrepAos<W>::Q];
+#pragma unroll
+    for (int q = 0; q < PrepAos<W>::Q; q++) {
+        const uint4 v = a[q];
+        w[4 * q] = v.x;
+        w[4 * q + 1] = v.y;
+        w[4 * q + 2] = v.z;
+        w[4 * q + 3] = v.w;
+    }
+    const Soa ds(wk.digits, PV_DIGIT_ROWS, wk.stride);
+#pragma unroll
+    for (int q = 0; q < 8 + Bc2<W>::POS; q++) ds.st(q, i, w[q]);
+    wk.flags[i] = w[8 + Bc2<W>::POS];
+}
+
 // Wide fixed-base comb rows (comb.h PV_BC2_*): row j = entries 0..PV_BC2_ENT-1 of [d 2^(W j)] B,
 // 8 uint4 each, LDS-staged like DevBStage; 64-bit entry index (the table is ~10.7 GB at W = 24).
 template <uint32_t ENT>
@@ -1806,11 +1902,32 @@ __device__ __forceinline__ uint32_t pv_xcd_block() {
 
 // Second half: Q = acc + [k](-A) from the key's comb table (32 additions, no doublings), projective
 // Q to q rows 0..29; the key's own libsodium checks are folded into flags[i] here.
-__device__ __forceinline__ void pv_comb_a_slot(const Work& wk, const KeyWork& kw, uint32_t i, uint4* stg_wave) {
+__device__ __forceinline__ void pv_comb_a_from(const Work& wk, const KeyWork& kw, uint32_t i, const ge_p3& acc,
+                                               uint4* stg_wave) {
     const uint32_t id = kw.skey[i];  // comb index
     const uint32_t cslot = kw.comb_cslot[id];
     const uint4* ktab = cslot != PV_EMPTY ? kw.kc_tab + (uint64_t)cslot * PV_COMB_POS * PV_COMB_ENT * 10
                                           : kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10;
+    const Soa qs(wk.q, 40, wk.stride);
+    const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
+    fe X, Y, Z;
+#if PV_COMB_PIPELINE
+    pv_comb_a_xyz_staged(X, Y, Z, acc, DevCombStage{ktab, stg_wave, threadIdx.x & 63u}, dig);
+#else
+    const DevCombRows arows{const_cast<uint4*>(ktab)};
+    pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
+#endif
+    if (kw.key_flag[id] == 0) wk.flags[i] = 0;
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        qs.st(q, i, X.v[q]);
+        qs.st(10 + q, i, Y.v[q]);
+        qs.st(20 + q, i, Z.v[q]);
+    }
+}
+
+// comb_a after a separate pv_comb_b_kernel: acc = [S]B from q rows 0..39 (or qb, PV_COMB_B_EARLY).
+__device__ __forceinline__ void pv_comb_a_slot(const Work& wk, const KeyWork& kw, uint32_t i, uint4* stg_wave) {
     const uint32_t S = (uint32_t)wk.stride;
     const Soa qs(wk.q, 40, wk.stride);
     ge_p3 acc;
@@ -1843,21 +1960,8 @@ __device__ __forceinline__ void pv_comb_a_slot(const Work& wk, const KeyWork& kw
         acc.T.v[q] = qs.ld(30 + q, i);
     }
 #endif
-    const DevDigits dig{wk.digits, S, i};
-    fe X, Y, Z;
-#if PV_COMB_PIPELINE
-    pv_comb_a_xyz_staged(X, Y, Z, acc, DevCombStage{ktab, stg_wave, threadIdx.x & 63u}, dig);
-#else
-    const DevCombRows arows{const_cast<uint4*>(ktab)};
-    pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
-#endif
-    if (kw.key_flag[id] == 0) wk.flags[i] = 0;
-#pragma unroll
-    for (int q = 0; q < 10; q++) {
-        qs.st(q, i, X.v[q]);
-        qs.st(10 + q, i, Y.v[q]);
-        qs.st(20 + q, i, Z.v[q]);
-    }
+    (void)S;
+    pv_comb_a_from(wk, kw, i, acc, stg_wave);
 }
 
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kernel(uint64_t n, Work wk, KeyWork kw,
@@ -1868,6 +1972,31 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
     __shared__ uint4 stg[PV_BLOCK / 64][10][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     pv_comb_a_slot(wk, kw, i, &stg[wv][0][0]);
+}
+
+// [S]B and [k](-A) of a comb slot in ONE kernel (PV_COMB_FUSED): the 10 niels additions from the wide
+// fixed-base comb (random 128 B entries in HBM, LDS-staged one addition ahead in the first 8 rows of
+// the wave's staging area) run inside the issue-bound comb kernel, where the other waves of the SIMD
+// cover their fetch latency, instead of as a latency-bound kernel of their own between comb_prep and
+// the per-key tables; and acc never round-trips through q. The kernel then starts as soon as the
+// per-key tables are built.
+#ifndef PV_COMB_FUSED
+#define PV_COMB_FUSED 1
+#endif
+template <int W>
+__global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kernel(uint64_t n, Work wk, KeyWork kw,
+                                                                                const uint4* __restrict__ bcomb,
+                                                                                Gate gate) {
+    if (!gate.keyed() || gate.off()) return;
+    const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
+    if (i >= gate.ncomb()) return;
+    __shared__ uint4 stg[PV_BLOCK / 64][10][64];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
+    ge_p3 acc;
+    pv_comb_b_acc_w<Bc2<W>::POS>(acc, DevB2Stage<Bc2<W>::ENT>{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
+                                 [&](int j) { return dig.fb(j); });
+    pv_comb_a_from(wk, kw, i, acc, &stg[wv][0][0]);
 }
 
 // Kernel 3: encode Q for PV_ENC_BATCH requests per lane with one shared inversion, compare with R,
@@ -1963,7 +2092,7 @@ struct Ctx {
     hipEvent_t ev_verdict_copied = nullptr;  // pv_verify_batch: verdicts back (an admission may follow)
     hipStream_t last_stream = nullptr;
     uint32_t* d_btab = nullptr;
-    Work work{nullptr, nullptr, nullptr, nullptr, 0};
+    Work work{nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
     KeyWork kw{};
     bool last_keyed = false;  // the most recent chunk ran the dedup / split kernels
     bool slots_dirty = true;  // the key hash table / need masks may hold entries (cleared before use)
@@ -1976,6 +2105,7 @@ struct Ctx {
     uint4* d_bcomb = nullptr;  // fixed-base comb T_B (radix 65536; latency path)
     uint4* d_bc2 = nullptr;    // wide fixed-base comb T_B2 (radix 2^W; comb path's [S]B)
     int bc2_w = PV_BC2_W;      // its radix: PV_BC2_W, or 16 when d_bc2 aliases d_bcomb (fallback)
+    uint32_t prep_lds_pad = PV_PREP_LDS_PAD;  // dynamic LDS per comb_prep workgroup (occupancy cap)
     int path = PV_PATH_AUTO;
     // host-entry staging
     uint8_t* h_stage = nullptr;  // pinned
@@ -2368,8 +2498,13 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #endif
             PV_HIP(hipEventRecord(g_ctx.ev_straus_done, ss), PV_ERR_LAUNCH);
-            PV_LAUNCH_BC2(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                               d_pk + 32 * c0, g_ctx.work, kw, gate);
+#if PV_PREP_REQ_ORDER
+            PV_LAUNCH_BC2(pv_comb_prep_req_kernel, dim3(grid), dim3(PV_BLOCK), g_ctx.prep_lds_pad, stream, d_sm,
+                          d_off + c0, m, d_pk + 32 * c0, g_ctx.work, kw, gate);
+#else
+            PV_LAUNCH_BC2(pv_comb_prep_kernel, dim3(grid), dim3(PV_BLOCK), g_ctx.prep_lds_pad, stream, d_sm,
+                          d_off + c0, m, d_pk + 32 * c0, g_ctx.work, kw, gate);
+#endif
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             // a small chunk's sparse table fill (needs the chain's bases and the need masks comb_prep
             // writes) runs on fstream after the full fill; for a large chunk it exits at once
@@ -2379,10 +2514,15 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                                0, g_ctx.fstream, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
+#if PV_PREP_REQ_ORDER
+            // the per-request results to slot-ordered rows, while the key stream finishes the tables
+            PV_LAUNCH_BC2(pv_comb_digits_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, g_ctx.work, kw, gate);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#endif
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
 #if PV_COMB_B_EARLY
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_b_done, 0), PV_ERR_LAUNCH);
-#else
+#elif !PV_COMB_FUSED
             // [S]B while the key stream finishes the tables, then join
             PV_LAUNCH_BC2(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
                                gate);
@@ -2390,7 +2530,13 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
 #endif
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
+#if PV_COMB_FUSED && !PV_COMB_B_EARLY
+            // [S]B + [k](-A) in one kernel as soon as the tables are built
+            PV_LAUNCH_BC2(pv_comb_ab_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, g_ctx.d_bc2,
+                          gate);
+#else
             hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
+#endif
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_straus_done, 0), PV_ERR_LAUNCH);
         } else {
@@ -2444,6 +2590,7 @@ int pv_fail(int code, const std::string& msg) { return fail(code, msg); }
 extern "C" {
 
 int pv_abi_version(void) { return PV_ABI_VERSION; }
+uint32_t pv_build_flags(void) { return (PV_COMB_FUSED && !PV_COMB_B_EARLY) ? PV_BUILD_COMB_FUSED : 0u; }
 
 int pv_device_count(void) {
     int n = 0;
@@ -2517,6 +2664,7 @@ int ctx_init(int device) {
     PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * PV_DIGIT_ROWS * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
     PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 40 * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&g_ctx.work.aos, S * PV_PREP_AOS_QMAX * 16), PV_ERR_ALLOC);
 #if PV_COMB_B_EARLY
     PV_HIP(hipMalloc((void**)&g_ctx.work.qb, S * 160), PV_ERR_ALLOC);
 #endif
@@ -2614,6 +2762,7 @@ int ctx_init(int device) {
     }
     PV_HIP(hipHostMalloc((void**)&g_ctx.h_zc_verdict, PV_ZC_MAX_REQ, hipHostMallocCoherent | hipHostMallocPortable),
            PV_ERR_ALLOC);
+    if (const char* pad = getenv("PV_PREP_LDS_PAD")) g_ctx.prep_lds_pad = (uint32_t)atoi(pad);  // A/B knob
     g_ctx.device = device;
     return PV_OK;
 }
@@ -2635,6 +2784,7 @@ void ctx_free() {
     if (g_ctx.work.flags) (void)hipFree(g_ctx.work.flags);
     if (g_ctx.work.q) (void)hipFree(g_ctx.work.q);
     if (g_ctx.work.qb) (void)hipFree(g_ctx.work.qb);
+    if (g_ctx.work.aos) (void)hipFree(g_ctx.work.aos);
     for (void* p : {(void*)g_ctx.kw.slot, (void*)g_ctx.kw.slot_id, (void*)g_ctx.kw.slot_cnt, (void*)g_ctx.kw.req_key,
                     (void*)g_ctx.kw.req_rank, (void*)g_ctx.kw.nkeys,
                     (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_cid, (void*)g_ctx.kw.comb_key,

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("PLENUM_AMD_LIB", os.path.join(_HERE, "libplenum_verif
 PV_OK = 0
 PV_BLOB_SLACK = 256
 PV_ABI_VERSION = 1
+PV_BUILD_COMB_FUSED = 1  # pv_build_flags(): [S]B and [k](-A) of the comb path in one kernel
 
 PV_STAGES = ("keys", "prep", "table", "msm", "encode")  # PV_STAGE_* order
 PV_PATH_AUTO, PV_PATH_STRAUS, PV_PATH_COMB, PV_PATH_LATENCY = 0, 1, 2, 3
@@ -27,6 +28,7 @@ _c_u64p = ctypes.POINTER(ctypes.c_uint64)
 _c_u32p = ctypes.POINTER(ctypes.c_uint32)
 SIGNATURES = {
     "pv_abi_version": (ctypes.c_int, []),
+    "pv_build_flags": (ctypes.c_uint32, []),
     "pv_device_count": (ctypes.c_int, []),
     "pv_init": (ctypes.c_int, [ctypes.c_int]),
     "pv_shutdown": (None, []),
@@ -168,6 +170,11 @@ def verify_sm_batch(blob, offsets, pks):
     bits = np.zeros((n + 7) // 8, dtype=np.uint8)
     check(L.pv_verify_batch(_ptr(blob), _ptr(offsets), n, _ptr(pks), _ptr(bits)), "pv_verify_batch")
     return np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+
+
+def comb_fused():
+    """True if the library computes the comb path's [S]B and [k](-A) in one kernel (pv_comb_ab_kernel)."""
+    return bool(lib().pv_build_flags() & PV_BUILD_COMB_FUSED)
 
 
 def last_zero_copy():

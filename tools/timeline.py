@@ -34,7 +34,7 @@ def main():
         raise SystemExit("no %s in the trace (columns: %s)" % (a.first_kernel, cols))
     if a.summary:
         keys = ("pv_key_insert", "pv_key_assign_kernel", "pv_key_scan_kernel", "pv_key_chain_lp_kernel", "pv_key_fill_kernel",
-                "pv_comb_b_kernel", "pv_comb_a_kernel", "pv_msm_kernel", "pv_encode_kernel")
+                "pv_comb_b_kernel", "pv_comb_a_kernel", "pv_comb_ab_kernel", "pv_msm_kernel", "pv_encode_kernel")
         print("row    span   " + " ".join("%8s" % k.replace("pv_", "").replace("_kernel", "")[:8] for k in keys)
               + "  comb_a_start")
         for j, s in enumerate(starts):
@@ -47,7 +47,7 @@ def main():
                 for k in keys:
                     if name.endswith(k) or name.startswith(k) or name.startswith("void " + k):
                         dur[k] = dur.get(k, 0.0) + (en - st) / 1e3
-                if "pv_comb_a_kernel" in name:
+                if "pv_comb_a_kernel" in name or "pv_comb_ab_kernel" in name:
                     ca = (st - t0) / 1e3
             print("%5d %7.1f " % (s, span) + " ".join("%8.1f" % dur.get(k, 0.0) for k in keys) + "  %8.1f" % ca)
         return
