@@ -75,8 +75,11 @@ static constexpr int PV_BLOCK = 256;
 // Dynamic LDS requested by every pv_comb_prep_kernel workgroup, unused: it caps the kernel's residency
 // so that the key chain, launched beside it on the key stream, finds a wave slot on every SIMD at
 // once instead of waiting for prep workgroups to retire (env PV_PREP_LDS_PAD overrides at pv_init).
+// 41,984 B: 3 workgroups per CU (126 KB of the 160 KB), 3 prep waves per SIMD leave the chain's wave a
+// slot from the start -- A/B (profiles/r04/ab_pad.txt): chain 0.40 -> 0.31 ms in-step, comb kernel
+// starts 0.83 -> 0.79 ms, step -2 %; 54 KB (2 per CU) slows the prep more than it helps
 #ifndef PV_PREP_LDS_PAD
-#define PV_PREP_LDS_PAD 0
+#define PV_PREP_LDS_PAD 41984
 #endif
 static constexpr uint64_t PV_CHUNK = 1ull << 20;  // requests per launch sequence (workspace ~1.8 GB)
 static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tables hold (10.8 GB)
@@ -107,6 +110,9 @@ static constexpr uint32_t PV_ALLCOMB_CHUNK = 262144;
 // part competes with the next chain part for the SIMDs and each part is a launch of its own.
 #ifndef PV_CHAIN_PARTS
 #define PV_CHAIN_PARTS 1
+#endif
+#ifndef PV_DIRECT_FILL  // large chunks: fill on the key stream right behind the chain (no fstream hop)
+#define PV_DIRECT_FILL 1
 #endif
 static_assert(32 % PV_CHAIN_PARTS == 0, "PV_CHAIN_PARTS must divide the 32 comb positions");
 #ifndef PV_LP_CHAIN_BLOCKS
@@ -2373,6 +2379,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         kw.lat_choice = dev_choice ? 1u : 0u;
         kw.kc_tab = g_ctx.kc.d_tab;
         const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
+        const bool direct_fill = PV_CHAIN_MODE == 2 && PV_CHAIN_PARTS == 1 && PV_DIRECT_FILL && m > PV_SPARSE_CHUNK;
         if (keyed) {
             // the hash table and need masks are left empty by the previous keyed chunk (unpermute and
             // sparse fill kernels); after an enqueue failure they may not be, and are cleared here
@@ -2436,6 +2443,9 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
             // overlapped with the per-request prep on the main stream
             PV_HIP(hipEventRecord(g_ctx.ev_keys_ready, stream), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(g_ctx.kstream, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
+            // a chunk above PV_SPARSE_CHUNK never fills sparsely: chain and fill back to back on kstream
+            // and the tables-ready event right after the fill (no event hop to fstream, no gated
+            // sparse-fill launch in the dependency chain of the comb kernel)
             // the chain runs in PV_CHAIN_PARTS launches of consecutive positions; the fill of a part
             // runs on fstream as soon as its chain part is done, beside the chain of the next part
 #if PV_CHAIN_MODE == 2
@@ -2445,7 +2455,16 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
 #endif
             const uint64_t items = (uint64_t)limit * (PV_COMB_POS / parts) * PV_COMB_BLOCKS;
             const unsigned fgrid = (unsigned)std::min<uint64_t>((items + PV_BLOCK - 1) / PV_BLOCK, 4096);
-            for (int part = 0; part < parts; part++) {
+            if (direct_fill) {  // one part, no sparse fill possible: the fill follows the chain on kstream
+                hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(limit, PV_LP_CHAIN_BLOCKS)), dim3(64),
+                                   0, g_ctx.kstream, d_pk + 32 * c0, kw, gate, 0, PV_COMB_POS);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+                hipLaunchKernelGGL(pv_key_fill_kernel, dim3(fgrid), dim3(PV_BLOCK), 0, g_ctx.kstream, kw, gate, 0,
+                                   PV_COMB_POS);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+                PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.kstream), PV_ERR_LAUNCH);
+            }
+            for (int part = 0; part < parts && !direct_fill; part++) {
                 const int lo = part * PV_COMB_POS / parts, hi = (part + 1) * PV_COMB_POS / parts;
 #if PV_CHAIN_MODE == 2
                 hipLaunchKernelGGL(pv_key_chain_lp_kernel, dim3(std::min<uint32_t>(limit, PV_LP_CHAIN_BLOCKS)), dim3(64),
@@ -2506,14 +2525,16 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                           d_off + c0, m, d_pk + 32 * c0, g_ctx.work, kw, gate);
 #endif
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            // a small chunk's sparse table fill (needs the chain's bases and the need masks comb_prep
-            // writes) runs on fstream after the full fill; for a large chunk it exits at once
-            PV_HIP(hipEventRecord(g_ctx.ev_prep_done, stream), PV_ERR_LAUNCH);
-            PV_HIP(hipStreamWaitEvent(g_ctx.fstream, g_ctx.ev_prep_done, 0), PV_ERR_LAUNCH);
-            hipLaunchKernelGGL(pv_key_fill_sparse_kernel, dim3(PV_ALLCOMB_KEYS * PV_COMB_POS / PV_BLOCK), dim3(PV_BLOCK),
-                               0, g_ctx.fstream, kw, gate);
-            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
+            if (!direct_fill) {
+                // a small chunk's sparse table fill (needs the chain's bases and the need masks comb_prep
+                // writes) runs on fstream after the full fill; for a large chunk it exits at once
+                PV_HIP(hipEventRecord(g_ctx.ev_prep_done, stream), PV_ERR_LAUNCH);
+                PV_HIP(hipStreamWaitEvent(g_ctx.fstream, g_ctx.ev_prep_done, 0), PV_ERR_LAUNCH);
+                hipLaunchKernelGGL(pv_key_fill_sparse_kernel, dim3(PV_ALLCOMB_KEYS * PV_COMB_POS / PV_BLOCK),
+                                   dim3(PV_BLOCK), 0, g_ctx.fstream, kw, gate);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+                PV_HIP(hipEventRecord(g_ctx.ev_tables_ready, g_ctx.fstream), PV_ERR_LAUNCH);
+            }
 #if PV_PREP_REQ_ORDER
             // the per-request results to slot-ordered rows, while the key stream finishes the tables
             PV_LAUNCH_BC2(pv_comb_digits_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, g_ctx.work, kw, gate);
