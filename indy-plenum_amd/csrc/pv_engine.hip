@@ -2164,6 +2164,7 @@ struct Ctx {
     uint64_t d_mg_words = 0;
     uint64_t* h_mg = nullptr;
     uint64_t h_mg_words = 0;
+    const uint32_t* last_nkeys = nullptr;  // split counters of the most recent keyed chunk
 };
 
 // One context per device. The single-device ABI (pv_init, pv_verify_batch, ...) works on the device
@@ -2287,6 +2288,12 @@ int ensure_events(int count) {
 int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const uint8_t* d_pk, uint64_t* d_verdict,
                   hipStream_t stream);
 
+int lane_alloc_buffers(Work& w, KeyWork& kw);
+void lane_free_buffers(Work& w, KeyWork& kw);
+
+int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, const uint8_t* d_pk,
+                 uint64_t* d_verdict, hipStream_t stream, bool latency, bool dev_choice, int evb);
+
 // A kernel instantiated per wide-comb radix (Bc2<W>), launched for the radix pv_init chose.
 #define PV_LAUNCH_BC2(k, ...)                                                                      \
     do {                                                                                           \
@@ -2333,7 +2340,18 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
         if (rc) return rc;
         g_ctx.ev_used = evb + NE * nchunks;
     }
-    for (int c = 0; c < nchunks; c++) {
+    int rc = PV_OK;
+    for (int c = 0; c < nchunks && rc == PV_OK; c++)
+        rc = launch_chunk(c, n, d_sm, d_off, d_pk, d_verdict, stream, latency, dev_choice, evb);
+    return rc;
+}
+
+// Chunk c of the batch on `stream` (the workspace is the context's; key / fill / side streams join it).
+int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, const uint8_t* d_pk,
+                 uint64_t* d_verdict, hipStream_t stream, bool latency, bool dev_choice, int evb) {
+    constexpr int NE = PV_NSTAGES + 1;
+    const uint64_t cap = g_ctx.work.stride;
+    {
         const uint64_t c0 = (uint64_t)c * cap;
         const uint64_t m = std::min<uint64_t>(cap, n - c0);
         const unsigned grid = (unsigned)((m + PV_BLOCK - 1) / PV_BLOCK);
@@ -2353,7 +2371,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                                    d_verdict + c0 / 64, g_ctx.verdict_zeroed, stream, nullptr);
             if (rc) return rc;
             if ((rc = mark(PV_STAGE_ENCODE)) || (rc = mark(PV_NSTAGES))) return rc;
-            continue;
+            return PV_OK;
         }
         // Path split (measured round-1 costs on MI355X): a key's comb table costs ~0.47 us of device
         // time (chain + 4,128-entry fill) and then saves ~10 ns per request against the Straus
@@ -2370,6 +2388,7 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
                             (m >= PV_KEYED_MIN || g_ctx.keyed_hint || dev_choice || kc_active));
         Gate gate{nullptr, nullptr};
         g_ctx.last_keyed = keyed;
+        if (keyed) g_ctx.last_nkeys = g_ctx.kw.nkeys;
         KeyWork kw = g_ctx.kw;
         kw.min_req = g_ctx.path == PV_PATH_COMB ? 1u : (uint32_t)PV_COMB_MIN_REQ;
         kw.kc_on = kc_active ? 1u : 0u;
@@ -2633,6 +2652,59 @@ int check_device_index(int device, const char* who) {
     return PV_OK;
 }
 
+// The per-lane workspace: per-request rows (Work) and the keyed path's tables (KeyWork), ~15 GB.
+int lane_alloc_buffers(Work& w, KeyWork& kw) {
+    const uint64_t S = PV_CHUNK;
+    w.stride = S;
+    PV_HIP(hipMalloc((void**)&w.atab, S * PV_ATAB_ENT * 160), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&w.digits, S * PV_DIGIT_ROWS * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&w.flags, S * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&w.q, S * 40 * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&w.aos, S * PV_PREP_AOS_QMAX * 16), PV_ERR_ALLOC);
+#if PV_COMB_B_EARLY
+    PV_HIP(hipMalloc((void**)&w.qb, S * 160), PV_ERR_ALLOC);
+#endif
+    const uint64_t H = 2 * S;
+    kw.hmask = (uint32_t)(H - 1);
+    kw.kcap = PV_KEY_CAP;
+    kw.seed = (uint32_t)std::random_device{}() | 1u;
+    PV_HIP(hipMalloc((void**)&kw.slot, H * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.slot_id, H * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.slot_cnt, H * 4 * PV_RANK_SUB), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.req_key, S * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.req_rank, S * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.nkeys, PV_SPLIT_ALLOC_WORDS * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.key_owner, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
+    PV_HIP(hipMalloc((void**)&kw.key_cid, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
+    PV_HIP(hipMalloc((void**)&kw.comb_key, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_PTS * 160), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.key_count, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
+    PV_HIP(hipMalloc((void**)&kw.key_cursor, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
+    PV_HIP(hipMalloc((void**)&kw.slot_req, S * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.req_pos, S * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.skey, S * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.sverdict, S / 64 * 8), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.key_cslot, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
+    PV_HIP(hipMalloc((void**)&kw.comb_cslot, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMalloc((void**)&kw.need, (uint64_t)PV_ALLCOMB_KEYS * PV_COMB_POS * 5 * 4), PV_ERR_ALLOC);
+    PV_HIP(hipMemset(kw.comb_cslot, 0xFF, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+    return PV_OK;
+}
+
+void lane_free_buffers(Work& w, KeyWork& kw) {
+    for (void* p : {(void*)w.atab, (void*)w.digits, (void*)w.flags, (void*)w.q, (void*)w.qb, (void*)w.aos,
+                    (void*)kw.slot, (void*)kw.slot_id, (void*)kw.slot_cnt, (void*)kw.req_key, (void*)kw.req_rank,
+                    (void*)kw.nkeys, (void*)kw.key_owner, (void*)kw.key_cid, (void*)kw.comb_key, (void*)kw.key_flag,
+                    (void*)kw.bases, (void*)kw.ctab, (void*)kw.key_count, (void*)kw.key_cursor, (void*)kw.slot_req,
+                    (void*)kw.req_pos, (void*)kw.skey, (void*)kw.sverdict, (void*)kw.key_cslot, (void*)kw.comb_cslot,
+                    (void*)kw.need})
+        if (p) (void)hipFree(p);
+    w = Work{nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+    kw = KeyWork{};
+}
+
 // Builds g_ctxs[device] (caller: g_mus[device] held, DevScope(device) active, context not built yet):
 // streams and events, the fixed-base tables, the workspace. Sets the calling thread's HIP device.
 int ctx_init(int device) {
@@ -2679,44 +2751,9 @@ int ctx_init(int device) {
     pv_build_b_table(bt.data());
     PV_HIP(hipMalloc((void**)&g_ctx.d_btab, bt.size() * 4), PV_ERR_ALLOC);
     PV_HIP(hipMemcpy(g_ctx.d_btab, bt.data(), bt.size() * 4, hipMemcpyHostToDevice), PV_ERR_ALLOC);
-    const uint64_t S = PV_CHUNK;
-    g_ctx.work.stride = S;
-    PV_HIP(hipMalloc((void**)&g_ctx.work.atab, S * PV_ATAB_ENT * 160), PV_ERR_ALLOC);
-    PV_HIP(hipMalloc((void**)&g_ctx.work.digits, S * PV_DIGIT_ROWS * 4), PV_ERR_ALLOC);
-    PV_HIP(hipMalloc((void**)&g_ctx.work.flags, S * 4), PV_ERR_ALLOC);
-    PV_HIP(hipMalloc((void**)&g_ctx.work.q, S * 40 * 4), PV_ERR_ALLOC);
-    PV_HIP(hipMalloc((void**)&g_ctx.work.aos, S * PV_PREP_AOS_QMAX * 16), PV_ERR_ALLOC);
-#if PV_COMB_B_EARLY
-    PV_HIP(hipMalloc((void**)&g_ctx.work.qb, S * 160), PV_ERR_ALLOC);
-#endif
     {
-        KeyWork& kw = g_ctx.kw;
-        const uint64_t H = 2 * S;
-        kw.hmask = (uint32_t)(H - 1);
-        kw.kcap = PV_KEY_CAP;
-        kw.seed = (uint32_t)std::random_device{}() | 1u;
-        PV_HIP(hipMalloc((void**)&kw.slot, H * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.slot_id, H * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.slot_cnt, H * 4 * PV_RANK_SUB), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.req_key, S * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.req_rank, S * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.nkeys, PV_SPLIT_ALLOC_WORDS * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_owner, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
-        PV_HIP(hipMalloc((void**)&kw.key_cid, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
-        PV_HIP(hipMalloc((void**)&kw.comb_key, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_flag, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.bases, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_PTS * 160), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.ctab, (uint64_t)kw.kcap * PV_COMB_POS * PV_COMB_ENT * 160), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_count, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
-        PV_HIP(hipMalloc((void**)&kw.key_cursor, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
-        PV_HIP(hipMalloc((void**)&kw.slot_req, S * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.req_pos, S * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.skey, S * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.sverdict, S / 64 * 8), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.key_cslot, (S + 64 * PV_NSEG) * 4), PV_ERR_ALLOC);  // key ids: segment-major
-        PV_HIP(hipMalloc((void**)&kw.comb_cslot, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMalloc((void**)&kw.need, (uint64_t)PV_ALLCOMB_KEYS * PV_COMB_POS * 5 * 4), PV_ERR_ALLOC);
-        PV_HIP(hipMemset(kw.comb_cslot, 0xFF, (uint64_t)kw.kcap * 4), PV_ERR_ALLOC);
+        int rc = lane_alloc_buffers(g_ctx.work, g_ctx.kw);
+        if (rc) return rc;
         std::vector<uint32_t> bc((size_t)PV_BCOMB_POS * PV_BCOMB_ENT * PV_BCOMB_STRIDE);
         {
             ge_p3 base[PV_BCOMB_POS];
@@ -2800,22 +2837,9 @@ void ctx_free() {
     if (g_ctx.h_stage) (void)hipHostFree(g_ctx.h_stage);
     if (g_ctx.d_stage) (void)hipFree(g_ctx.d_stage);
     if (g_ctx.d_btab) (void)hipFree(g_ctx.d_btab);
-    if (g_ctx.work.atab) (void)hipFree(g_ctx.work.atab);
-    if (g_ctx.work.digits) (void)hipFree(g_ctx.work.digits);
-    if (g_ctx.work.flags) (void)hipFree(g_ctx.work.flags);
-    if (g_ctx.work.q) (void)hipFree(g_ctx.work.q);
-    if (g_ctx.work.qb) (void)hipFree(g_ctx.work.qb);
-    if (g_ctx.work.aos) (void)hipFree(g_ctx.work.aos);
-    for (void* p : {(void*)g_ctx.kw.slot, (void*)g_ctx.kw.slot_id, (void*)g_ctx.kw.slot_cnt, (void*)g_ctx.kw.req_key,
-                    (void*)g_ctx.kw.req_rank, (void*)g_ctx.kw.nkeys,
-                    (void*)g_ctx.kw.key_owner, (void*)g_ctx.kw.key_cid, (void*)g_ctx.kw.comb_key,
-                    (void*)g_ctx.kw.key_flag, (void*)g_ctx.kw.bases,
-                    (void*)g_ctx.kw.ctab, (void*)g_ctx.d_bcomb,
-                    (void*)(g_ctx.d_bc2 != g_ctx.d_bcomb ? g_ctx.d_bc2 : nullptr), (void*)g_ctx.kw.key_count,
-                    (void*)g_ctx.kw.key_cursor, (void*)g_ctx.kw.slot_req, (void*)g_ctx.kw.req_pos,
-                    (void*)g_ctx.kw.skey, (void*)g_ctx.kw.sverdict, (void*)g_ctx.kw.key_cslot,
-                    (void*)g_ctx.kw.comb_cslot, (void*)g_ctx.kw.need})
-        if (p) (void)hipFree(p);
+    lane_free_buffers(g_ctx.work, g_ctx.kw);
+    if (g_ctx.d_bcomb) (void)hipFree(g_ctx.d_bcomb);
+    if (g_ctx.d_bc2 && g_ctx.d_bc2 != g_ctx.d_bcomb) (void)hipFree(g_ctx.d_bc2);
     for (hipEvent_t e : g_ctx.ev) (void)hipEventDestroy(e);
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     if (g_ctx.kstream) (void)hipStreamDestroy(g_ctx.kstream);
@@ -2895,7 +2919,8 @@ int pv_last_path(int* path, uint32_t* nkeys) {
     if (g_ctx.last_keyed) {
         PV_HIP(hipStreamSynchronize(g_ctx.stream), PV_ERR_LAUNCH);
         PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
-        PV_HIP(hipMemcpy(u, g_ctx.kw.nkeys, sizeof(u), hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpy(u, g_ctx.last_nkeys ? g_ctx.last_nkeys : g_ctx.kw.nkeys, sizeof(u), hipMemcpyDeviceToHost),
+               PV_ERR_LAUNCH);
     }
     if (nkeys) *nkeys = u[PV_SPLIT_KEYS];
     const bool lat = g_ctx.last_latency || (g_ctx.last_keyed && u[PV_SPLIT_LAT] != 0);
