@@ -913,14 +913,13 @@ __global__ __launch_bounds__(PV_INS_THREADS) void pv_key_insert_lds_kernel(const
     __syncthreads();
     const uint32_t i0 = blockIdx.x * PV_INS_REQS;
     uint32_t* cnt = kw.slot_cnt + (uint64_t)((blockIdx.x & (PV_RANK_SUB - 1u))) * (kw.hmask + 1ull);
-    uint32_t hs[PV_INS_PER_THREAD], es[PV_INS_PER_THREAD], lr[PV_INS_PER_THREAD];
+    uint32_t es[PV_INS_PER_THREAD], lr[PV_INS_PER_THREAD];
 #pragma unroll
     for (uint32_t u = 0; u < PV_INS_PER_THREAD; u++) {
         const uint32_t i = i0 + u * PV_INS_THREADS + t;
         es[u] = PV_EMPTY;
         if (i >= n) continue;
         const uint32_t h = pv_key_slot(pk, kw, i);
-        hs[u] = h;
         kw.req_key[i] = h;
         uint32_t e = (h * 2654435761u) >> (32 - 12);  // log2(PV_INS_LT)
         for (int probe = 0; probe < 64; probe++) {
@@ -1021,9 +1020,15 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_cache_probe_kernel(const uint
 #ifndef PV_SCAN_WAVE
 #define PV_SCAN_WAVE 1
 #endif
+static constexpr uint32_t PV_SCAN_THREADS = 1024;  // pv_key_scan_kernel's block
 #if PV_SCAN_WAVE
 // Wave scans by shuffles, then the 16 wave totals (two barriers instead of Hillis-Steele's twenty).
+// Written for 64-lane waves and exactly 16 of them (the 1,024-thread pv_key_scan_kernel).
+#if defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "pv_block_scan assumes wave64 (gfx950)"
+#endif
 __device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
+    static_assert(PV_SCAN_THREADS == 16 * 64, "16 wave64 totals");
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint32_t x = v;  // inclusive scan within the wave
 #pragma unroll
@@ -1066,6 +1071,7 @@ __device__ uint32_t pv_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
 // order, every other key's requests the slots [CS, n). Threads own contiguous id ranges; three
 // passes over key_count: comb index, slot totals, cursors.
 static constexpr uint32_t PV_SCAN_REG = 16;  // key counts a scan thread keeps in registers
+// launched with exactly PV_SCAN_THREADS threads (pv_block_scan's 16 wave totals)
 __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uint32_t* __restrict__ kc_flags) {
     __shared__ uint32_t part[1024];
     // the key ids are segment-major (pv_key_assign_kernel): v-th key in segment order = id vid(v)
@@ -2454,7 +2460,8 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             }
             gate = Gate{kw.nkeys, kw.slot_req};
             // key-sorted slot order: comb keys' requests first, then the Straus requests
-            hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(1024), 0, stream, kw, (const uint32_t*)g_ctx.kc.d_flags);
+            hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(PV_SCAN_THREADS), 0, stream, kw,
+                               (const uint32_t*)g_ctx.kc.d_flags);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_scatter_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
