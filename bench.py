@@ -359,6 +359,16 @@ def config1_legs(wire, procs=16):
     return one
 
 
+def _pmc_kernel(kernels, name):
+    """The PMC summary entry of kernel `name` (template instances are keyed "void name<W>")."""
+    if name in kernels:
+        return kernels[name]
+    for k, v in kernels.items():
+        if k.startswith("void %s<" % name):
+            return v
+    return {}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present:
     2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md: on gfx950 FETCH_SIZE counts half the bytes of
@@ -369,7 +379,7 @@ def pmc_traffic(kernel):
     try:
         with open(p) as f:
             d = json.load(f)
-        k = d.get("kernels", {}).get(kernel, {})
+        k = _pmc_kernel(d.get("kernels", {}), kernel)
         return k.get("hbm_bytes_per_launch_corrected", k.get("hbm_bytes_per_launch"))
     except Exception:
         return None
@@ -383,7 +393,7 @@ def pmc_valu_issue(kernel, cus=256):
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
-            k = json.load(f)["kernels"][kernel]
+            k = _pmc_kernel(json.load(f)["kernels"], kernel)
         c = k["counters_per_dispatch"]
         return round(c["SQ_INSTS_VALU"] / (k["median_dispatch_s_under_pmc"] * k["eff_clock_GHz"] * 1e9 * cus), 3)
     except Exception:

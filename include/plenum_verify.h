@@ -62,8 +62,9 @@ extern "C" {
 int pv_abi_version(void);
 /* Build configuration of the library's kernels (bit set = compiled in):
  *   PV_BUILD_COMB_FUSED  the keyed comb path computes [S]B and [k](-A) in ONE kernel
- *                        (pv_comb_ab_kernel, the MSM stage) instead of pv_comb_b_kernel (TABLE stage)
- *                        + pv_comb_a_kernel (MSM stage) */
+ *                        (pv_comb_ab_kernel, the MSM stage) for chunks above 262,144 requests instead
+ *                        of pv_comb_b_kernel (TABLE stage) + pv_comb_a_kernel (MSM stage); smaller
+ *                        chunks keep the two kernels */
 #define PV_BUILD_COMB_FUSED 1u
 uint32_t pv_build_flags(void);
 

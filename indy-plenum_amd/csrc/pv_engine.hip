@@ -1995,6 +1995,13 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
 #ifndef PV_COMB_FUSED
 #define PV_COMB_FUSED 1
 #endif
+// ... for chunks above this many requests. Below it the two-kernel form stays: a small chunk's [S]B
+// kernel is a latency-bound chain of 10 dependent HBM lookups that the split form hides beside the
+// table fill, while the fused kernel would add it after the fill (4,096-32,768-request calls were
+// 0.08-0.12 ms slower fused).
+#ifndef PV_FUSED_MIN_REQ
+#define PV_FUSED_MIN_REQ 262144
+#endif
 template <int W>
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                 const uint4* __restrict__ bcomb,
@@ -2567,23 +2574,23 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #endif
             if ((rc = mark(PV_STAGE_TABLE))) return rc;
+            const bool fused = PV_COMB_FUSED && !PV_COMB_B_EARLY && m > PV_FUSED_MIN_REQ;
 #if PV_COMB_B_EARLY
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_b_done, 0), PV_ERR_LAUNCH);
-#elif !PV_COMB_FUSED
-            // [S]B while the key stream finishes the tables, then join
-            PV_LAUNCH_BC2(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
-                               gate);
-            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+#else
+            if (!fused) {  // [S]B while the key stream finishes the tables, then join
+                PV_LAUNCH_BC2(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
+                              gate);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            }
 #endif
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
-#if PV_COMB_FUSED && !PV_COMB_B_EARLY
-            // [S]B + [k](-A) in one kernel as soon as the tables are built
-            PV_LAUNCH_BC2(pv_comb_ab_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, g_ctx.d_bc2,
-                          gate);
-#else
-            hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
-#endif
+            if (fused)  // [S]B + [k](-A) in one kernel as soon as the tables are built
+                PV_LAUNCH_BC2(pv_comb_ab_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, g_ctx.d_bc2,
+                              gate);
+            else
+                hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_straus_done, 0), PV_ERR_LAUNCH);
         } else {

@@ -248,9 +248,11 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
     const bool eq = lp_final_check(c, K, QA, s_sb[lane], dec.X, dec.Y);
     const bool ok = eq && key_ok && r_ok && s_sig_ok != 0;
     if constexpr (ZC) {
-        // a coherent pinned byte the host spins on while the kernel runs (pv_spin_verdict_bytes):
-        // published with release semantics at system scope
-        if (lane == 0) __hip_atomic_store(&vbytes[r], (uint8_t)(ok ? 1u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // a coherent (fine-grained) pinned byte the host spins on while the kernel runs
+        // (pv_spin_verdict_bytes): a system-scope atomic store goes straight to host memory; relaxed,
+        // since the byte itself is the only datum the host reads (a release would write back the
+        // whole L2 once per request)
+        if (lane == 0) __hip_atomic_store(&vbytes[r], (uint8_t)(ok ? 1u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     } else {
         if (lane == 0 && ok) atomicOr(&verdict[r >> 6], 1ull << (r & 63));
     }
@@ -477,9 +479,11 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
     const bool eq = lp_final_check(c, K, QA, s_part[0][lane], dec.X, dec.Y);
     const bool ok = eq && key_ok && r_ok && s_sig_ok != 0;
     if constexpr (ZC) {
-        // a coherent pinned byte the host spins on while the kernel runs (pv_spin_verdict_bytes):
-        // published with release semantics at system scope
-        if (lane == 0) __hip_atomic_store(&vbytes[r], (uint8_t)(ok ? 1u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // a coherent (fine-grained) pinned byte the host spins on while the kernel runs
+        // (pv_spin_verdict_bytes): a system-scope atomic store goes straight to host memory; relaxed,
+        // since the byte itself is the only datum the host reads (a release would write back the
+        // whole L2 once per request)
+        if (lane == 0) __hip_atomic_store(&vbytes[r], (uint8_t)(ok ? 1u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     } else {
         if (lane == 0 && ok) atomicOr(&verdict[r >> 6], 1ull << (r & 63));
     }
