@@ -549,6 +549,59 @@ LP_FN void lp_build_a_table(const LpLane& c, const LpConsts& K, const lu& negA, 
     }
 }
 
+// [2^n] P without P's x: on -x^2 + y^2 = 1 + d x^2 y^2, x^2 = (y^2 - 1) / (d y^2 + 1) is a function of
+// y, so doubling maps y to a function of y alone, and x to x times a function of y:
+//   y' = (d a^2 + 2ab - b^2) / (-d a^2 + 2d ab + b^2),  x' / x = 2YZ (d a + b) / (d a^2 + b^2)
+// for y = Y / Z, a = Y^2, b = Z^2 (both denominators are nonzero for every y: -1/d is not a fourth power
+// and the doubling is complete). The chain can therefore start from the encoding's y at once,
+// while x is still being decompressed, and x enters once at the end (lp_ydbl_finish): three
+// multiplications a doubling (rows [a, b, YZ, U num], [a^2, b^2, ab, d a], [d a^2, d ab, YZ (d a + b),
+// W den]) against two for lp_dbl, off the critical path. State rows [Y, Z, U, W] with x_n = x_0 U / W
+// (the last step's num / den still pending in num_den rows 0 / 1).
+struct LpYChain {
+    lu st;       // [Y, Z, U, W]
+    lu num_den;  // [num, den, -, -] of the last doubling (applied by the next one / the finish)
+};
+LP_FN LpYChain lp_ydbl_chain(const LpLane& c, const LpConsts& K, const lu& y0, int n) {
+    const lu one = K.one;
+    lu Y = y0, Z = one, U = one, W = one, num = one, den = one;
+    for (int i = 0; i < n; i++) {
+        const lu m1 = lp_mul(c, c.rows(Y, Z, Y, U), c.rows(Y, Z, Z, num));  // [a, b, YZ, U num]
+        lu a, b, yz, u1;
+        lp_allrows(m1, a, b, yz, u1);
+        const lu m2 = lp_mul(c, c.rows(a, b, a, K.d), c.rows(a, b, b, a));  // [a^2, b^2, ab, d a]
+        lu a2, b2, ab, da;
+        lp_allrows(m2, a2, b2, ab, da);
+        const lu m3 = lp_mul(c, c.rows(da, da, yz, W), c.rows(a, b, da + b, den));  // [d a^2, d ab, YZ (d a + b), W den]
+        lu da2, dab, nm, w1;
+        lp_allrows(m3, da2, dab, nm, w1);
+        Y = lp_carry1(c, lp_sub(c, da2 + ab + ab, b2));
+        Z = lp_carry1(c, lp_sub(c, dab + dab + b2, da2));
+        U = u1;
+        W = w1;
+        num = nm + nm;
+        den = da2 + b2;
+    }
+    LpYChain o;
+    o.st = c.rows(Y, Z, U, W);
+    o.num_den = c.rows(num, den, 0u, 0u);
+    return o;
+}
+// The ext point [2^n] P of the chain once P's x is known: x0 = P's affine x in every row.
+// (x0 U Z : Y W : Z W : x0 U Y), U and W with the pending num / den applied.
+LP_FN lu lp_ydbl_finish(const LpLane& c, const LpConsts& K, const LpYChain& ch, const lu& x0) {
+    lu Y, Z, U, W, num, den, t0, t1;
+    lp_allrows(ch.st, Y, Z, U, W);
+    lp_allrows(ch.num_den, num, den, t0, t1);
+    const lu uw = lp_mul(c, c.rows(U, W, U, W), c.rows(num, den, num, den));  // [Uf, Wf, Uf, Wf]
+    lu Uf, Wf;
+    lp_allrows(uw, Uf, Wf, t0, t1);
+    const lu g = lp_mul(c, c.rows(Uf, Y, Z, Uf), c.rows(x0, Wf, Wf, x0));  // [G = x0 Uf, Y Wf, Z Wf, G]
+    lu G, YW, ZW, t2;
+    lp_allrows(g, G, YW, ZW, t2);
+    return lp_mul(c, c.rows(G, YW, ZW, G), c.rows(Z, K.one, K.one, Y));
+}
+
 // [k](-A) by regular signed radix-16 windows: 63 x 4 doublings + 64 table additions. digit(i) =
 // the i-th signed digit (wave-uniform), load(e) = the table entry for digit e.
 template <class Digit, class Load>
@@ -714,7 +767,26 @@ LP_FN bool lp_t_small(const LpLane& c, const lu& st) {
     return lp_ballot(bad) == 0;
 }
 
-LP_FN void lp_halfsize(const LpLane& c, pv_halfk& h, const uint32_t k[8]) {
+// PV_LP_SPLIT_53 = 1: a Lehmer block reads 53 leading bits (exact doubles), takes one division per
+// quotient and accepts it under Jebelean's conditions (~25 bits per block: ~5 blocks); 0: sc_halfsize's
+// 31-bit blocks with Knuth's two-division test (~9 blocks). Both settle only true quotients, so both
+// give sc_halfsize's split.
+#ifndef PV_LP_SPLIT_53
+#define PV_LP_SPLIT_53 1
+#endif
+// 1 / x to 1 ulp (v_rcp_f32 on the device)
+LP_FN float lp_rcpf(float x) {
+#if LP_DEVICE
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+#ifndef LP_SPLIT_MARK  // phase timer hook of microbench/lp_split_lat.hip (no-op otherwise)
+#define LP_SPLIT_MARK(i)
+#endif
+// stats (measurement only, nullptr otherwise): as sc_halfsize's
+LP_FN void lp_halfsize(const LpLane& c, pv_halfk& h, const uint32_t k[8], uint32_t* stats = nullptr) {
     lu st = 0u;
 #pragma unroll
     for (int i = 0; i < 9; i++) {
@@ -728,7 +800,59 @@ LP_FN void lp_halfsize(const LpLane& c, pv_halfk& h, const uint32_t k[8]) {
         const uint64_t nz = lp_ballot(lp_ne(st, 0u));
         const uint32_t r1nz = (uint32_t)(nz >> 16) & 0x1FFu;
         if ((r1nz >> 5) == 0 && (lp_readlane(st, 20) >> 3) == 0) break;
+        if (stats) stats[0]++;
+        LP_SPLIT_MARK(0);
         const int w = 31 - __builtin_clz((uint32_t)nz & 0x1FFu);  // >= 4 (r0 > r1 >= 2^131)
+#if PV_LP_SPLIT_53
+        // 53 leading bits of r0 (2^52 <= xh < 2^53) and r1 at the same shift e, exact in doubles
+        const uint32_t a1 = lp_readlane(st, w), a0 = lp_readlane(st, w - 1), a2 = lp_readlane(st, w - 2);
+        const uint32_t b1 = lp_readlane(st, 16 + w), b0 = lp_readlane(st, 15 + w), b2 = lp_readlane(st, 14 + w);
+        const int s = 43 - (int)__builtin_clz(a1);  // bits of (a1:a0:a2) = 96 - clz(a1); keep 53 (s = 12..43)
+        const uint64_t ah = ((uint64_t)a1 << 32) | a0, bh = ((uint64_t)b1 << 32) | b0;
+        const uint64_t xi = s <= 32 ? (ah << (32 - s)) | ((uint64_t)a2 >> s) : ah >> (s - 32);
+        const uint64_t yi = s <= 32 ? (bh << (32 - s)) | ((uint64_t)b2 >> s) : bh >> (s - 32);
+        const int e = 32 * (w - 2) + s;  // >= 79 here (r0 >= 2^132)
+        const double ythr = e >= 130 ? 1.0 : (double)(1ull << (130 - e));  // stop the block above 2^130
+        // Euclid on the digits, (x, y) = (r_n, r_{n+1}) estimates, with the cosequence rows as sign-free
+        // magnitudes: row j is (+P, -N) for even j, (-N, +P) for odd j, and P_j = P_{j-2} + q N_{j-1},
+        // N_j = N_{j-2} + q P_{j-1}. The true r_j = x_j 2^e + delta_j with -N_j 2^e < delta_j < P_j 2^e,
+        // so the digit quotient is the true one when the new remainder is >= N_j and the old one
+        // exceeds it by >= N_{j-1} + P_j (Jebelean's conditions); the two slots alternate roles.
+        double x = (double)xi, y = (double)yi, Px = 1.0, Nx = 0.0, Py = 1.0, Ny = 0.0;
+        int n = 0;
+#define LP_QSTEP(U, V, PU, NU, PV, NV)                                                                       \
+    {                                                                                                        \
+        /* |estimate - quotient| <= 1 for quotients < 2^21 (f32 operands, 1-ulp reciprocal) */              \
+        double q = (double)__builtin_floorf((float)U * lp_rcpf((float)V));                     \
+        double nr = __builtin_fma(-q, V, U);                                                                 \
+        /* branch-free fix-up (uniform values: selects, not jumps) */                                       \
+        const bool lo_ = nr < 0.0;                                                                           \
+        q = lo_ ? q - 1.0 : q;                                                                               \
+        nr = lo_ ? nr + V : nr;                                                                              \
+        const bool hi_ = nr >= V;                                                                            \
+        q = hi_ ? q + 1.0 : q;                                                                               \
+        nr = hi_ ? nr - V : nr;                                                                              \
+        const double nP = __builtin_fma(q, NV, PU), nN = __builtin_fma(q, PV, NU);                           \
+        const bool ok_ = (q < 2097152.0) & (nr >= ythr) & (nr >= nN) & (V - nr >= NV + nP) &                 \
+                         (nP + nN < 2147483648.0);                                                           \
+        if (!ok_) break;                                                                                     \
+        U = nr;                                                                                              \
+        PU = nP;                                                                                             \
+        NU = nN;                                                                                             \
+        n++;                                                                                                 \
+        if (stats) stats[1]++;                                                                               \
+    }
+        for (int it = 0; it < 48; it++) {
+            LP_QSTEP(x, y, Px, Nx, Py, Ny)
+            LP_QSTEP(y, x, Py, Ny, Px, Nx)
+        }
+#undef LP_QSTEP
+        // rows n (A, B) and n + 1 (C, D): slot x always holds the even row, slot y the odd one
+        const double Pe = Px, Ne = Nx, Po = Py, No = Ny;
+        // even row (P, -N), odd row (-N, P); n even: (A, B) even, (C, D) odd; n odd: the reverse
+        const double A = (n & 1) ? -No : Pe, B = (n & 1) ? Po : -Ne;
+        const double C = (n & 1) ? Pe : -No, D = (n & 1) ? -Ne : Po;
+#else
         const uint32_t a1 = lp_readlane(st, w), a0 = lp_readlane(st, w - 1);
         const uint32_t b1 = lp_readlane(st, 16 + w), b0 = lp_readlane(st, 15 + w);
         const int sh = 33 - (int)__builtin_clz(a1);
@@ -753,12 +877,16 @@ LP_FN void lp_halfsize(const LpLane& c, pv_halfk& h, const uint32_t k[8]) {
             D = (int32_t)nD;
             xh = yh;
             yh = (int32_t)ny;
+            if (stats) stats[1]++;
         }
+#endif
+        LP_SPLIT_MARK(1);
         if (B == 0) {
             // one exact step: q from the top three words, then fixed by whole additions of r0
-            const uint32_t a2 = lp_readlane(st, w - 2), b2 = lp_readlane(st, 14 + w);
-            const double qd = ((double)a1 * 4294967296.0 + (double)a0 + (double)a2 / 4294967296.0) /
-                              ((double)b1 * 4294967296.0 + (double)b0 + (double)b2 / 4294967296.0);
+            const uint32_t ta1 = lp_readlane(st, w), ta0 = lp_readlane(st, w - 1), ta2 = lp_readlane(st, w - 2);
+            const uint32_t tb1 = lp_readlane(st, 16 + w), tb0 = lp_readlane(st, 15 + w), tb2 = lp_readlane(st, 14 + w);
+            const double qd = ((double)ta1 * 4294967296.0 + (double)ta0 + (double)ta2 / 4294967296.0) /
+                              ((double)tb1 * 4294967296.0 + (double)tb0 + (double)tb2 / 4294967296.0);
             if (!(qd < 2147483647.0)) {
                 bad = true;
                 break;
@@ -768,14 +896,17 @@ LP_FN void lp_halfsize(const LpLane& c, pv_halfk& h, const uint32_t k[8]) {
             if ((int32_t)lp_readlane(st, 24) < 0) st = lp_mat_update(c, st, 1, 0, 1, 1);
             else if (!lp_pair_ordered(c, st)) st = lp_mat_update(c, st, 1, 0, -1, 1);
         } else {
-            st = lp_mat_update(c, st, A, B, C, D);
+            st = lp_mat_update(c, st, (int64_t)A, (int64_t)B, (int64_t)C, (int64_t)D);
         }
+        LP_SPLIT_MARK(2);
         bad |= !lp_pair_ordered(c, st) || !lp_t_small(c, st);
+        LP_SPLIT_MARK(3);
     }
     // ---- exact single steps until r1 < 2^128 with t1 odd
     for (int it = 0; it < PV_HALF_MAXIT && !bad; it++) {
         const uint64_t nz = lp_ballot(lp_ne(st, 0u));
         if ((((uint32_t)(nz >> 16) & 0x1FFu) >> 4) == 0 && (lp_readlane(st, 48) & 1u)) break;
+        if (stats) stats[2]++;
         const int w = 31 - __builtin_clz(((uint32_t)nz & 0x1FFu) | 1u);
         if (w < 2 || ((nz >> 16) & 0x1FFu) == 0) {
             bad = true;

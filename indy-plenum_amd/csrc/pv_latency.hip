@@ -344,11 +344,19 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
 
     if (wave >= 2) {
         if (!cached) {
+            // the 68 doublings run on y alone from the encoding (lp_ydbl_chain), beside wave 0's
+            // decompression; x enters once it is published
+            lu yw[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) yw[q] = wave == 2 ? in.A[q] : in.R[q];
+            const LpYChain ch = lp_ydbl_chain(c, K, lp_from_words(c, yw), 4 * PV_LAT4_SPLIT);
+            LAT_STAMP(wave == 2 ? 7 : 15);
             // wait for wave 0's decompression (a workgroup's waves are co-resident: it progresses)
             while (s_pts_ready == 0u) __builtin_amdgcn_s_sleep(2);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            lu P = wave == 2 ? lu(s_pa[lane]) : lu(s_pr[lane]);
-            for (int j = 0; j < 4 * PV_LAT4_SPLIT; j++) P = lp_dbl(c, P);
+            lu x0, t1, t2, t3;
+            lp_allrows(wave == 2 ? lu(s_pa[lane]) : lu(s_pr[lane]), x0, t1, t2, t3);  // ext rows [x, y, 1, xy]
+            const lu P = lp_ydbl_finish(c, K, ch, x0);
             lp_build_a_table(c, K, P, [&](int j, const lu& q) { s_tab[wave][j + 8][lane] = q; });
         }
         __syncthreads();  // 1: split, tables ready

@@ -323,6 +323,51 @@ int hc_lp_halfsize(const uint8_t* k, uint8_t* k1, uint8_t* k2, int* neg) {
     *neg = h.neg;
     return h.fallback;
 }
+// lp_ydbl_chain + lp_ydbl_finish (the four-wave latency kernel's y-only [2^n] chains) against n
+// lp_dbl steps of the decompressed point, for -A (row 0) and R (row 1) of lp_decompress_ar: bit r of
+// the result is set when row r's two points are equal projectively; -1 if either does not decompress.
+int hc_lp_ydbl_check(const uint8_t* a_enc, const uint8_t* r_enc, int n) {
+    uint32_t wa[8], wr[8];
+    load_words(wa, a_enc);
+    load_words(wr, r_enc);
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    lu sw[8];
+    for (int q = 0; q < 8; q++) sw[q] = lp_sel(lp_eq(c.row & 1u, 1u), wr[q], wa[q]);
+    const LpDecomp dec = lp_decompress_ar(c, K, sw);
+    if (!dec.ok_a || !dec.ok_r) return -1;
+    int mask = 0;
+    for (int which = 0; which < 2; which++) {
+        const lu P = lp_ext_from_xy(c, K, dec.X, dec.Y, which);
+        lu Q = P;
+        for (int i = 0; i < n; i++) Q = lp_dbl(c, Q);
+        lu yw[8];
+        for (int q = 0; q < 8; q++) yw[q] = which ? wr[q] : wa[q];
+        const LpYChain ch = lp_ydbl_chain(c, K, lp_from_words(c, yw), n);
+        lu x0, t1, t2, t3;
+        lp_allrows(P, x0, t1, t2, t3);
+        const lu R = lp_ydbl_finish(c, K, ch, x0);
+        bool same = true;
+        for (int r = 0; r < 4; r += (r == 1 ? 2 : 1)) {  // X, Y and T against Z
+            fe a, b, d;
+            fe_mul(a, lp_row_fe(Q, r), lp_row_fe(R, 2));
+            fe_mul(b, lp_row_fe(R, r), lp_row_fe(Q, 2));
+            fe_sub(d, a, b);
+            same &= fe_iszero(d);
+        }
+        mask |= same ? 1 << which : 0;
+    }
+    return mask;
+}
+// lp_halfsize's counts for one scalar: [0] Lehmer blocks, [1] quotients settled inside them, [2] exact steps
+void hc_lp_halfsize_stats(const uint8_t* k, uint32_t* stats) {
+    uint32_t kw[8];
+    load_words(kw, k);
+    const LpLane c = LpLane::make();
+    pv_halfk h;
+    stats[0] = stats[1] = stats[2] = 0;
+    lp_halfsize(c, h, kw, stats);
+}
 
 // The half-size Straus path as the device runs it: pv_prepare_half (checks, +-A, -R', split of k,
 // k2 S mod L), the [j]PA and [j](-R') tables, [k2 S]B from pv_comb_b_acc_w<16> over the radix-65536

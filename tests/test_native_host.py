@@ -407,3 +407,23 @@ def test_lp_halfsize_matches_per_lane_split(hc):
             fb = fn(b, k1, k2, ctypes.byref(neg))
             outs.append((k1.raw, k2.raw, neg.value, fb))
         assert outs[0] == outs[1], k
+
+
+def test_lp_ydbl_chain_matches_doublings(hc):
+    """The four-wave latency kernel's [2^68] chains run on y alone (lp_ydbl_chain: y' and the x ratio
+    as functions of y) and take x at the end (lp_ydbl_finish): the same point as 68 lp_dbl steps of the
+    decompressed -A and R, with the limb bounds asserted, at random points and at x = 0 (y = +-1)."""
+    rng = random.Random(46)
+    encs = [(1).to_bytes(32, "little"), (P - 1).to_bytes(32, "little")]
+    encs += [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(400)]
+    tested = 0
+    for i, a in enumerate(encs):
+        r = encs[(i * 7 + 3) % len(encs)]
+        for n in ((68,) if i % 8 else (1, 2, 68)):
+            got = hc.hc_lp_ydbl_check(a, r, n)
+            if got == -1:
+                break
+            assert got == 3, (i, n)
+            tested += 1
+    assert tested >= 50
+

@@ -5,6 +5,7 @@ with PLENUM_AMD_LIB. Verifies a 1-request batch `reps` times on the forced laten
 for the last call, block 0's s_memrealtime stamps (100 MHz) relative to wave 0's start, in us:
   wave 0: 0 start, 1 decompression done, 2 tables done, 3 past barrier 1, 4 loop done,
           5 past barrier 2, 6 verdict written
+  waves 2, 3 (four-wave form): 14 start, 7 / 15 y-only chain done (lp_ydbl_chain)
   wave 1: 8 start, 9 k ready, 12 split done, 13 k2 S mod L done, 10 digits and comb entries ready,
           11 [S]B / [k2](-R') + [s2]B done
 """
