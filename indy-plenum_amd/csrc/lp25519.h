@@ -315,6 +315,60 @@ LP_FN lu lp_mul(const LpLane& c, const lu& f, const lu& g) {
 }
 LP_FN lu lp_sq(const LpLane& c, const lu& f) { return lp_mul(c, f, f); }
 
+// lp_mul for operands whose rows 2, 3 repeat rows 0, 1 (two elements, each held twice, as in the
+// decompression chain): rows 0, 1 sum the column terms i = 0..4 and rows 2, 3 the terms i = 5..9 (f
+// and the extended g pre-rotated by five limbs there), the halves are added across with one
+// v_permlane32_swap per word, and every row carries the full product: 5 term products per lane
+// instead of 10. Same bounds and output as lp_mul.
+LP_FN lu lp_mul_dual(const LpLane& c, const lu& f, const lu& g) {
+#if !LP_DEVICE
+    for (int l = 0; l < 32; l++) {
+        if ((l & 15) >= 10) continue;  // scratch lanes are never read
+        LP_CHECK(f.v[l] == f.v[l + 32] && g.v[l] == g.v[l + 32], "lp_mul_dual rows 2, 3 repeat rows 0, 1");
+        LP_CHECK(g.v[l] < ((l & 1) ? 0x8600000u : 0xD790000u), "lp_mul g operand");
+    }
+#endif
+    const lm hi = lp_ge(c.row, 2u);
+    // rows 0, 1 (as lp_mul): lanes 0..9 g, lanes m >= 10 19 g_{m-6}
+    const lu Y = lp_shr<6>(g) * 19u;
+    const lu X = lp_sel(c.kge10, Y, g);
+    // rows 2, 3: lane j < 5 19 g_{j+5}, 5 <= j < 10 g_{j-5}, m >= 12 19 g_{m-11}: row_ror:i (i <= 4) of
+    // it gives lane k the factor g_{(k-i-5) mod 10} (19 when wrapped) of term i + 5
+    const lu Xr = lp_sel(lp_lt(c.k, 5u), lp_shl<5>(g) * 19u, lp_sel(c.kge10, lp_shr<11>(g) * 19u, lp_shr<5>(g)));
+    // odd x odd terms doubled on the rotated operand: rows 0, 1 hold limb index = lane parity, rows
+    // 2, 3 the opposite; term i + 5 has f index parity opposite to i
+    const lu Xo = lp_sel(hi, Xr, X);                       // the operand undoubled ...
+    const lu Xd = Xo + Xo;                                 // ... and doubled
+    const lm odd_limb = lp_eq((c.k ^ lp_sel(hi, 1u, 0u)) & 1u, 1u);
+    const lu D = lp_sel(odd_limb, Xd, Xo);                 // odd limbs doubled
+    const lu Ev = lp_sel(hi, D, Xo);                        // even i (rows 2, 3: odd f index i + 5)
+    const lu Od = lp_sel(hi, Xo, D);                        // odd i (rows 2, 3: even f index)
+    const lu fr = lp_sel(hi, lp_shl<5>(f), f);             // row_newbcast:i gives f_i / f_{i+5}
+    lu64 acc = lp_mad(lp_bcast<0>(fr), Ev, lu64(0ull));
+    acc = lp_mad(lp_bcast<1>(fr), lp_ror<1>(Od), acc);
+    acc = lp_mad(lp_bcast<2>(fr), lp_ror<2>(Ev), acc);
+    acc = lp_mad(lp_bcast<3>(fr), lp_ror<3>(Od), acc);
+    acc = lp_mad(lp_bcast<4>(fr), lp_ror<4>(Ev), acc);
+    // + the other half's partial column (rows r and r ^ 2)
+    lu plo = lp_lo(acc), qlo = plo, phi = lp_hi(acc), qhi = phi;
+    lp_swap32(plo, qlo);
+    lp_swap32(phi, qhi);
+    acc = lp_join(phi, plo) + lp_join(qhi, qlo);
+    // carries as lp_mul
+    const lu64 cy = lp_shr64(acc, c.w);
+    const lu lo = lp_lo(acc) & c.mask;
+    const lu clo = lp_lo(cy), chi = lp_hi(cy);
+    const lu wlo = lp_shl<9>(clo), whi = lp_shl<9>(chi);
+    const lu64 w19 = lp_mad(wlo, 19u, lp_join(whi * 19u, 0u));
+    const lu64 in = lp_sel64(c.k0, w19, lp_join(lp_shr<1>(chi), lp_shr<1>(clo)));
+    const lu64 t = in + lp_wide(lo);
+    const lu cy2 = lp_lo(lp_shr64(t, c.w));
+    const lu l2 = lp_lo(t) & c.mask;
+    const lu h = l2 + lp_sel(c.k0, lp_shl<9>(cy2) * 19u, lp_shr<1>(cy2));
+    LP_BOUND(h, (1u << 26) + (1u << 23), "lp_mul_dual output");
+    return h;
+}
+
 // every row gets row r of x: o0 = row 0 in all rows, ... (3 permlane instructions)
 LP_FN void lp_allrows(const lu& x, lu& o0, lu& o1, lu& o2, lu& o3) {
     lu p = x, q = x;
@@ -327,34 +381,42 @@ LP_FN void lp_allrows(const lu& x, lu& o0, lu& o1, lu& o2, lu& o3) {
     lp_swap32(o1, o3);
 }
 
-// z^(2^252 - 3) in every row at once (libsodium's chain, as fe_pow22523)
+// DUAL: the operands' rows 2, 3 repeat rows 0, 1 (lp_mul_dual)
+template <bool DUAL>
+LP_FN lu lp_mulx(const LpLane& c, const lu& f, const lu& g) {
+    if constexpr (DUAL) return lp_mul_dual(c, f, g);
+    else return lp_mul(c, f, g);
+}
+template <bool DUAL = false>
 LP_FN lu lp_sqn(const LpLane& c, lu x, int n) {
-    for (int i = 0; i < n; i++) x = lp_sq(c, x);
+    for (int i = 0; i < n; i++) x = lp_mulx<DUAL>(c, x, x);
     return x;
 }
+// z^(2^252 - 3) in every row at once (libsodium's chain, as fe_pow22523)
+template <bool DUAL = false>
 LP_FN lu lp_pow22523(const LpLane& c, const lu& z) {
-    lu t0 = lp_sq(c, z);                 // z^2
-    lu t1 = lp_sqn(c, t0, 2);            // z^8
-    t1 = lp_mul(c, z, t1);               // z^9
-    t0 = lp_mul(c, t0, t1);              // z^11
-    lu t2 = lp_sq(c, t0);                // z^22
-    t1 = lp_mul(c, t1, t2);              // z^(2^5 - 1)
-    t2 = lp_sqn(c, t1, 5);
-    t1 = lp_mul(c, t2, t1);              // z^(2^10 - 1)
-    t2 = lp_sqn(c, t1, 10);
-    t2 = lp_mul(c, t2, t1);              // z^(2^20 - 1)
-    lu t3 = lp_sqn(c, t2, 20);
-    t2 = lp_mul(c, t3, t2);              // z^(2^40 - 1)
-    t2 = lp_sqn(c, t2, 10);
-    t1 = lp_mul(c, t2, t1);              // z^(2^50 - 1)
-    t2 = lp_sqn(c, t1, 50);
-    t2 = lp_mul(c, t2, t1);              // z^(2^100 - 1)
-    t3 = lp_sqn(c, t2, 100);
-    t2 = lp_mul(c, t3, t2);              // z^(2^200 - 1)
-    t2 = lp_sqn(c, t2, 50);
-    t1 = lp_mul(c, t2, t1);              // z^(2^250 - 1)
-    t1 = lp_sqn(c, t1, 2);               // z^(2^252 - 4)
-    return lp_mul(c, t1, z);             // z^(2^252 - 3)
+    lu t0 = lp_mulx<DUAL>(c, z, z);              // z^2
+    lu t1 = lp_sqn<DUAL>(c, t0, 2);              // z^8
+    t1 = lp_mulx<DUAL>(c, z, t1);                // z^9
+    t0 = lp_mulx<DUAL>(c, t0, t1);               // z^11
+    lu t2 = lp_mulx<DUAL>(c, t0, t0);            // z^22
+    t1 = lp_mulx<DUAL>(c, t1, t2);               // z^(2^5 - 1)
+    t2 = lp_sqn<DUAL>(c, t1, 5);
+    t1 = lp_mulx<DUAL>(c, t2, t1);               // z^(2^10 - 1)
+    t2 = lp_sqn<DUAL>(c, t1, 10);
+    t2 = lp_mulx<DUAL>(c, t2, t1);               // z^(2^20 - 1)
+    lu t3 = lp_sqn<DUAL>(c, t2, 20);
+    t2 = lp_mulx<DUAL>(c, t3, t2);               // z^(2^40 - 1)
+    t2 = lp_sqn<DUAL>(c, t2, 10);
+    t1 = lp_mulx<DUAL>(c, t2, t1);               // z^(2^50 - 1)
+    t2 = lp_sqn<DUAL>(c, t1, 50);
+    t2 = lp_mulx<DUAL>(c, t2, t1);               // z^(2^100 - 1)
+    t3 = lp_sqn<DUAL>(c, t2, 100);
+    t2 = lp_mulx<DUAL>(c, t3, t2);               // z^(2^200 - 1)
+    t2 = lp_sqn<DUAL>(c, t2, 50);
+    t1 = lp_mulx<DUAL>(c, t2, t1);               // z^(2^250 - 1)
+    t1 = lp_sqn<DUAL>(c, t1, 2);                 // z^(2^252 - 4)
+    return lp_mulx<DUAL>(c, t1, z);              // z^(2^252 - 3)
 }
 
 // The 10 limbs of row r as a scalar fe (uniform values: v_readlane).
@@ -471,15 +533,15 @@ struct LpDecomp {
 LP_FN LpDecomp lp_decompress_ar(const LpLane& c, const LpConsts& K, const lu s[8]) {
     LpDecomp o;
     const lu y = lp_from_words(c, s);
-    lu u = lp_sq(c, y);
-    lu v = lp_mul(c, u, K.d);
+    lu u = lp_mul_dual(c, y, y);
+    lu v = lp_mul_dual(c, u, K.d);
     u = lp_carry1(c, lp_sub(c, u, K.one));  // u = y^2 - 1
     v = lp_carry1(c, v + K.one);              // v = d y^2 + 1
-    lu v3 = lp_mul(c, lp_sq(c, v), v);        // v^3
-    lu x = lp_mul(c, lp_mul(c, lp_sq(c, v3), v), u);  // u v^7
-    x = lp_pow22523(c, x);
-    x = lp_mul(c, lp_mul(c, x, v3), u);       // u v^3 (u v^7)^((p-5)/8)
-    const lu vxx = lp_mul(c, lp_sq(c, x), v);
+    lu v3 = lp_mul_dual(c, lp_mul_dual(c, v, v), v);        // v^3
+    lu x = lp_mul_dual(c, lp_mul_dual(c, lp_mul_dual(c, v3, v3), v), u);  // u v^7
+    x = lp_pow22523<true>(c, x);
+    x = lp_mul_dual(c, lp_mul_dual(c, x, v3), u);       // u v^3 (u v^7)^((p-5)/8)
+    const lu vxx = lp_mul_dual(c, lp_mul_dual(c, x, x), v);
     const lu chk_m = lp_sub(c, vxx, u), chk_p = vxx + u;
     const bool ok0 = lp_row_iszero(chk_m, 0), ok1 = lp_row_iszero(chk_m, 1);
     o.ok_a = ok0 || lp_row_iszero(chk_p, 0);

@@ -199,7 +199,13 @@ static constexpr uint32_t SC_8L[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa
 #define PV_HALF_MAXIT 64  // exact single steps (after the Lehmer blocks: ~3-12)
 #endif
 #ifndef PV_HALF_BLOCKS
-#define PV_HALF_BLOCKS 24  // Lehmer blocks (~9 needed from 2^255 to 2^131)
+#define PV_HALF_BLOCKS 24  // Lehmer blocks (~9 of 31 bits / ~6 of 53 bits from 2^255 to 2^131)
+#endif
+// PV_SC_SPLIT_53 = 1: Lehmer blocks on 53 leading bits with one division per quotient and
+// Jebelean's conditions (~6 blocks); 0: 31-bit blocks with Knuth's two-division test (~10 blocks).
+// Both settle only true quotients, so both give the same split.
+#ifndef PV_SC_SPLIT_53
+#define PV_SC_SPLIT_53 1
 #endif
 struct pv_halfk {
     uint32_t k1[8];  // |k1|
@@ -281,6 +287,15 @@ PV_HD bool mp_small168(const uint32_t t[8]) {
     return t[7] == s && t[6] == s && ((t[5] ^ s) >> 8) == 0;
 }
 
+// 1 / x to 1 ulp (v_rcp_f32 on the device)
+PV_HD float pv_rcpf(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+
 // floor(n / d) for 0 <= n < 2^31, 0 < d < 2^31 from a single-precision reciprocal estimate, fixed by
 // one exact step each way; ok = false (the caller ends its Lehmer block) for n < 0, d <= 0, a
 // quotient >= 2^20 or an estimate one step could not fix
@@ -326,6 +341,61 @@ PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8], uint32_t* stats = nullp
         const bool act = !bad && ((r1[4] >> 3) | r1[5] | r1[6] | r1[7]) != 0;
         if (pv_wave_all(!act)) break;
         if (!act) continue;
+#if PV_SC_SPLIT_53
+        // 53 leading bits (exact doubles), one division per quotient, Jebelean's conditions on the
+        // sign-free cosequence (the same block as lp25519.h lp_halfsize, per lane)
+        int w = 4;
+#pragma unroll
+        for (int i = 5; i < 8; i++) w = r0[i] ? i : w;
+        uint32_t a1 = 0, a0 = 0, a2 = 0, b1 = 0, b0 = 0, b2 = 0;
+#pragma unroll
+        for (int i = 4; i < 8; i++) {
+            a1 = i == w ? r0[i] : a1;
+            a0 = i == w ? r0[i - 1] : a0;
+            a2 = i == w ? r0[i - 2] : a2;
+            b1 = i == w ? r1[i] : b1;
+            b0 = i == w ? r1[i - 1] : b0;
+            b2 = i == w ? r1[i - 2] : b2;
+        }
+        const int s = 43 - (int)__builtin_clz(a1);
+        const uint64_t ah = ((uint64_t)a1 << 32) | a0, bh = ((uint64_t)b1 << 32) | b0;
+        const uint64_t xi = s <= 32 ? (ah << (32 - s)) | ((uint64_t)a2 >> s) : ah >> (s - 32);
+        const uint64_t yi = s <= 32 ? (bh << (32 - s)) | ((uint64_t)b2 >> s) : bh >> (s - 32);
+        const int e = 32 * (w - 2) + s;
+        const double ythr = e >= 130 ? 1.0 : (double)(1ull << (130 - e));
+        double x = (double)xi, y = (double)yi, Px = 1.0, Nx = 0.0, Py = 1.0, Ny = 0.0;
+        int n = 0;
+        bool go = true;
+#define SC_QSTEP(U, V, PU, NU, PV, NV)                                                                       \
+    {                                                                                                        \
+        double q = (double)__builtin_floorf((float)U * pv_rcpf((float)V));                                   \
+        double nr = __builtin_fma(-q, V, U);                                                                 \
+        const bool lo_ = nr < 0.0;                                                                           \
+        q = lo_ ? q - 1.0 : q;                                                                               \
+        nr = lo_ ? nr + V : nr;                                                                              \
+        const bool hi_ = nr >= V;                                                                            \
+        q = hi_ ? q + 1.0 : q;                                                                               \
+        nr = hi_ ? nr - V : nr;                                                                              \
+        const double nP = __builtin_fma(q, NV, PU), nN = __builtin_fma(q, PV, NU);                           \
+        go = (q < 2097152.0) & (nr >= ythr) & (nr >= nN) & (V - nr >= NV + nP) & (nP + nN < 2147483648.0);  \
+        if (go) {                                                                                            \
+            U = nr;                                                                                          \
+            PU = nP;                                                                                         \
+            NU = nN;                                                                                         \
+            n++;                                                                                             \
+            if (stats) stats[1]++;                                                                           \
+        }                                                                                                    \
+    }
+        for (int it = 0; it < 48; it++) {
+            if (pv_wave_all(!go)) break;
+            if (go) SC_QSTEP(x, y, Px, Nx, Py, Ny)
+            if (go) SC_QSTEP(y, x, Py, Ny, Px, Nx)
+        }
+#undef SC_QSTEP
+        // rows n (A, B) and n + 1 (C, D): slot x holds the even row (P, -N), slot y the odd (-N, P)
+        const int64_t A = (n & 1) ? -(int64_t)Ny : (int64_t)Px, B = (n & 1) ? (int64_t)Py : -(int64_t)Nx;
+        const int64_t C = (n & 1) ? (int64_t)Px : -(int64_t)Ny, D = (n & 1) ? -(int64_t)Nx : (int64_t)Py;
+#else
         // leading bits: xh = floor(r0 / 2^e), yh = floor(r1 / 2^e), 2^30 <= xh < 2^31 (r0 >= 2^131: w >= 4)
         int w = 4;
 #pragma unroll
@@ -372,6 +442,7 @@ PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8], uint32_t* stats = nullp
             yh = (int32_t)ny;
             if (stats) stats[1]++;
         }
+#endif
         if (stats) stats[0]++;
         if (B == 0) {
             // no quotient could be settled from the leading bits: one exact step below
@@ -406,7 +477,7 @@ PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8], uint32_t* stats = nullp
             }
         } else {
             uint32_t u[9], v[9], nr0[9], nr1[9], nt0[8], nt1[8], x[8], y[8];
-            mp_muls32<9>(u, r0, A);  // |A|, |B|, |C|, |D| < 2^15
+            mp_muls32<9>(u, r0, A);  // |A|, |B|, |C|, |D| < 2^31
             mp_muls32<9>(v, r1, B);
             mp_add<9>(nr0, u, v);
             mp_muls32<9>(u, r0, C);

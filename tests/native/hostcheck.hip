@@ -510,6 +510,15 @@ void hc_lp_pow22523(uint32_t* h, const uint32_t* f) {
     const LpLane c = LpLane::make();
     hc_rows_out(h, lp_pow22523(c, hc_rows_in(f)));
 }
+// lp_mul_dual / lp_pow22523<true>: rows 2, 3 of the inputs must repeat rows 0, 1
+void hc_lp_mul_dual(uint32_t* h, const uint32_t* f, const uint32_t* g) {
+    const LpLane c = LpLane::make();
+    hc_rows_out(h, lp_mul_dual(c, hc_rows_in(f), hc_rows_in(g)));
+}
+void hc_lp_pow22523_dual(uint32_t* h, const uint32_t* f) {
+    const LpLane c = LpLane::make();
+    hc_rows_out(h, lp_pow22523<true>(c, hc_rows_in(f)));
+}
 // group ops on an ext point given as 4 rows [X, Y, Z, T]
 void hc_lp_dbl(uint32_t* out, const uint32_t* p) {
     const LpLane c = LpLane::make();

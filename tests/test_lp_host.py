@@ -70,6 +70,32 @@ def test_lp_pow22523(hc):
             assert from_limbs(hr) % P == pow(z[r], (P - 5) // 8, P)
 
 
+def test_lp_mul_dual_matches_lp_mul(hc):
+    """lp_mul_dual (the decompression chain's product: rows 0, 1 sum column terms 0..4, rows 2, 3 terms
+    5..9 on operands pre-rotated by five limbs, halves added across with v_permlane32_swap) gives
+    lp_mul's limbs exactly, in all four rows, at the operand widths the chain forms; the dual
+    z^((p-5)/8) matches Python."""
+    rng = random.Random(5)
+    h, h2 = A40(), A40()
+    for it in range(400):
+        fb, gb = [(26.01, 26.01), (27.13, 27.13), (27.6, 26.6)][it % 3]
+        f = [rand_limbs(rng, fb) for _ in range(2)]
+        g = [rand_limbs(rng, gb) for _ in range(2)]
+        if it < 3:
+            f = [[int(2 ** (fb - (i & 1))) - 1 for i in range(10)]] * 2
+            g = [[int(2 ** (gb - (i & 1))) - 1 for i in range(10)]] * 2
+        fr, gr = rows_in(f + f), rows_in(g + g)
+        hc.hc_lp_mul(h, fr, gr)
+        hc.hc_lp_mul_dual(h2, fr, gr)
+        want = rows_out(h)
+        assert rows_out(h2) == [want[0], want[1], want[0], want[1]], it
+    for _ in range(4):
+        z = [rng.randrange(P) for _ in range(2)]
+        hc.hc_lp_pow22523_dual(h, rows_in(z + z))
+        for r, hr in enumerate(rows_out(h)):
+            assert from_limbs(hr) % P == pow(z[r & 1], (P - 5) // 8, P)
+
+
 def _decode(enc):
     """(x, y) of an Ed25519 encoding (RFC 8032 decompression)."""
     y = int.from_bytes(enc, "little") & (2 ** 255 - 1)

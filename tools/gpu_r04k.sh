@@ -13,3 +13,4 @@ done
 rm -rf gpurun_out/ablat
 SIZES=1,100,1000 timeout -k 10 400 bash tools/ab_latency.sh base lathead > $O/ab_latency.txt 2>&1 || exit $?
 cp -r gpurun_out/ablat $O/
+timeout -k 10 600 bash tools/ab_straus.sh 2 sc31 sc53 > $O/ab_straus.txt 2>&1 || exit $?
