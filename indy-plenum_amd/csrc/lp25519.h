@@ -844,10 +844,6 @@ LP_FN float lp_rcpf(float x) {
     return 1.0f / x;
 #endif
 }
-// PV_LP_SPLIT_SPEC = 1: the block's quotient steps commit through selects, one branch per four steps
-#ifndef PV_LP_SPLIT_SPEC
-#define PV_LP_SPLIT_SPEC 1
-#endif
 #ifndef LP_SPLIT_MARK  // phase timer hook of microbench/lp_split_lat.hip (no-op otherwise)
 #define LP_SPLIT_MARK(i)
 #endif
@@ -903,26 +899,6 @@ LP_FN void lp_halfsize(const LpLane& c, pv_halfk& h, const uint32_t k[8], uint32
                          (nP + nN < 2147483648.0);                                                           \
         LP_QCOMMIT(U, PU, NU)                                                                                \
     }
-#if PV_LP_SPLIT_SPEC
-        // steps committed by selects and a live flag (a failed step freezes the state, so the steps
-        // after it change nothing); one branch per four steps instead of one per step
-        bool live = true;
-#define LP_QCOMMIT(U, PU, NU)                                                                                \
-        const bool c_ = live & ok_;                                                                          \
-        U = c_ ? nr : U;                                                                                     \
-        PU = c_ ? nP : PU;                                                                                   \
-        NU = c_ ? nN : NU;                                                                                   \
-        n += c_ ? 1 : 0;                                                                                     \
-        live = c_;                                                                                           \
-        if (stats && c_) stats[1]++;
-        for (int it = 0; it < 24; it++) {
-            LP_QSTEP(x, y, Px, Nx, Py, Ny)
-            LP_QSTEP(y, x, Py, Ny, Px, Nx)
-            LP_QSTEP(x, y, Px, Nx, Py, Ny)
-            LP_QSTEP(y, x, Py, Ny, Px, Nx)
-            if (!live) break;
-        }
-#else
 #define LP_QCOMMIT(U, PU, NU)                                                                                \
         if (!ok_) break;                                                                                     \
         U = nr;                                                                                              \
@@ -934,7 +910,6 @@ LP_FN void lp_halfsize(const LpLane& c, pv_halfk& h, const uint32_t k[8], uint32
             LP_QSTEP(x, y, Px, Nx, Py, Ny)
             LP_QSTEP(y, x, Py, Ny, Px, Nx)
         }
-#endif
 #undef LP_QSTEP
 #undef LP_QCOMMIT
         // rows n (A, B) and n + 1 (C, D): slot x always holds the even row, slot y the odd one

@@ -40,16 +40,6 @@
 #ifndef PV_LAT_HALF
 #define PV_LAT_HALF 1
 #endif
-// PV_LAT_HYBRID_SHA = 1: wave 1's SHA-512 keeps the message schedule on the scalar unit
-// (pv_hash_k_hybrid); 0: all on the vector unit (pv_hash_k)
-#ifndef PV_LAT_HYBRID_SHA
-#define PV_LAT_HYBRID_SHA 1
-#endif
-#if PV_LAT_HYBRID_SHA
-#define PV_LAT_HASH_K pv_hash_k_hybrid
-#else
-#define PV_LAT_HASH_K pv_hash_k
-#endif
 // PV_LAT_TRACE (measurement builds only): block 0 stamps s_memrealtime (100 MHz) at its phase
 // boundaries into pv_lat_trace, read back by pv_debug_lat_trace.
 #ifdef PV_LAT_TRACE
@@ -146,7 +136,7 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 #pragma unroll
             for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
             uint32_t k[8];
-            PV_LAT_HASH_K(k, in, smlen, mw);
+            pv_hash_k(k, in, smlen, mw);
             LAT_STAMP(9);
             uint32_t e256[8], e16[8];
             sc_recode256(e256, k);
@@ -169,7 +159,7 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
             return;
         }
         uint32_t k[8], S[8];
-        PV_LAT_HASH_K(k, in, smlen, mw);
+        pv_hash_k(k, in, smlen, mw);
         LAT_STAMP(9);
         // every lane holds the same k: made uniform, the split runs on the scalar unit (short
         // dependent-instruction latency: this is one wave's serial chain)
@@ -389,7 +379,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
 #pragma unroll
             for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
             uint32_t k[8], e256[8];
-            PV_LAT_HASH_K(k, in, smlen, mw);
+            pv_hash_k(k, in, smlen, mw);
             sc_recode256(e256, k);
             if (lane == 0) {
 #pragma unroll
@@ -402,7 +392,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
             return;
         }
         uint32_t k[8], S[8];
-        PV_LAT_HASH_K(k, in, smlen, mw);
+        pv_hash_k(k, in, smlen, mw);
         LAT_STAMP(9);
 #pragma unroll
         for (int q = 0; q < 8; q++) {

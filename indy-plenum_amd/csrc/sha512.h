@@ -145,43 +145,4 @@ PV_HD void sha512_compress(uint64_t st[8], const uint64_t blk[16]) {
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-// The same compression for a wave whose lanes all hash the same block (the latency kernels' one
-// request per wave): blk must be wave-uniform, so the message schedule (and K + W) runs on the
-// scalar unit, while the working variables are pinned to VGPRs and the rounds run on the vector
-// unit -- the scalar instructions issue between the vector ones of the round chain instead of
-// adding ~40 % to it.
-PV_HD void sha512_compress_hybrid(uint64_t st[8], const uint64_t blk[16]) {
-    uint64_t w[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) w[i] = blk[i];
-    uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h));
-#endif
-#pragma unroll 1
-    for (int r = 0; r < 80; r += 16) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int i = r + j;
-            if (r > 0) {
-                const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-                const uint64_t s0 = ((w15 >> 1) | (w15 << 63)) ^ ((w15 >> 8) | (w15 << 56)) ^ (w15 >> 7);
-                const uint64_t s1 = ((w2 >> 19) | (w2 << 45)) ^ ((w2 >> 61) | (w2 << 3)) ^ (w2 >> 6);
-                w[i & 15] += s0 + w[(i - 7) & 15] + s1;
-            }
-            const uint64_t kw = PV_K512[i] + w[i & 15];
-            switch (j & 7) {
-                case 0: PV_SHA_ROUND(a, b, c, d, e, f, g, h, kw); break;
-                case 1: PV_SHA_ROUND(h, a, b, c, d, e, f, g, kw); break;
-                case 2: PV_SHA_ROUND(g, h, a, b, c, d, e, f, kw); break;
-                case 3: PV_SHA_ROUND(f, g, h, a, b, c, d, e, kw); break;
-                case 4: PV_SHA_ROUND(e, f, g, h, a, b, c, d, kw); break;
-                case 5: PV_SHA_ROUND(d, e, f, g, h, a, b, c, kw); break;
-                case 6: PV_SHA_ROUND(c, d, e, f, g, h, a, b, kw); break;
-                default: PV_SHA_ROUND(b, c, d, e, f, g, h, a, kw); break;
-            }
-        }
-    }
-    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
-}
 #undef PV_SHA_ROUND

@@ -520,53 +520,6 @@ PV_HD void pv_hash_k(uint32_t k[8], const pv_sig_words& in, uint64_t smlen, cons
     sc_reduce64(k, h);
 }
 
-// pv_hash_k for a wave whose lanes all verify the same request (the latency kernels): every input
-// word is made wave-uniform (readfirstlane) so the block words and the message schedule live in
-// SGPRs (sha512_compress_hybrid). Same result as pv_hash_k.
-PV_HD uint32_t pv_uniform(uint32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_readfirstlane(x);
-#else
-    return x;
-#endif
-}
-template <class MsgWord>
-PV_HD void pv_hash_k_hybrid(uint32_t k[8], const pv_sig_words& in, uint64_t smlen, const MsgWord& msgword) {
-    const uint32_t T = pv_uniform((uint32_t)smlen);
-    uint64_t st[8];
-    sha512_init(st);
-    const uint32_t nblocks = (T + 17 + 127) / 128;
-    for (uint32_t b = 0; b < nblocks; b++) {
-        uint64_t blk[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t q = 16 * b + j;
-            const uint64_t mv = msgword(q);
-            uint64_t raw = pv_pack64(pv_uniform((uint32_t)(mv >> 32)), pv_uniform((uint32_t)mv));
-            if (j < 8 && b == 0)  // block 0 only: R || A
-                raw = j < 4 ? pv_pack64(pv_uniform(in.R[2 * j + 1]), pv_uniform(in.R[2 * j]))
-                            : pv_pack64(pv_uniform(in.A[2 * (j - 4) + 1]), pv_uniform(in.A[2 * (j - 4)]));
-            const int32_t rem = (int32_t)T - (int32_t)(8 * q);
-            const uint32_t nb = rem < 0 ? 0u : (rem > 8 ? 8u : (uint32_t)rem);
-            const uint64_t mask = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
-            const uint64_t pad = (rem >= 0 && rem < 8) ? (0x80ull << (8 * rem)) : 0ull;
-            raw = (raw & mask) | pad;
-            uint64_t be = __builtin_bswap64(raw);
-            if (j == 15 && b == nblocks - 1) be = (uint64_t)T * 8;
-            blk[j] = be;
-        }
-        sha512_compress_hybrid(st, blk);
-    }
-    uint32_t h[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint64_t le = pv_bswap64(st[i]);
-        h[2 * i] = (uint32_t)le;
-        h[2 * i + 1] = (uint32_t)(le >> 32);
-    }
-    sc_reduce64(k, h);
-}
-
 // Stage 1 of a verification: the checks, A decompression and k. Returns false if any libsodium
 // pre-check rejects (the caller still runs the arithmetic on harmless data and masks the verdict).
 template <class MsgWord>

@@ -97,22 +97,6 @@ void hc_encode_batch(uint8_t* out, const uint32_t* xyz, int* use) {
 }
 int hc_enc_batch_size(void) { return PV_ENC_BATCH; }
 
-// k = SHA-512(R || A || M) mod L through the per-lane hash (hybrid = 0) or the latency kernels'
-// pv_hash_k_hybrid (message schedule on the scalar unit on the device); out: 32 bytes little-endian.
-void hc_hash_k(uint8_t* out, const uint8_t* sm, uint64_t smlen, const uint8_t* pk, int hybrid) {
-    std::vector<uint8_t> buf(smlen + 256, 0);  // PV_BLOB_SLACK
-    memcpy(buf.data(), sm, smlen);
-    pv_sig_words in;
-    memcpy(in.R, buf.data(), 32);
-    memcpy(in.S, buf.data() + 32, 32);
-    memcpy(in.A, pk, 32);
-    HostMsg mw{buf.data()};
-    uint32_t k[8];
-    if (hybrid) pv_hash_k_hybrid(k, in, smlen, mw);
-    else pv_hash_k(k, in, smlen, mw);
-    memcpy(out, k, 32);
-}
-
 // ---- keyed comb path on the host (comb.h): same code the comb kernels run
 struct HostBases {
     ge_p3* b;  // [32][PV_COMB_PTS]

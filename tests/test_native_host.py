@@ -426,21 +426,3 @@ def test_lp_ydbl_chain_matches_doublings(hc):
             assert got == 3, (i, n)
             tested += 1
     assert tested >= 50
-
-
-def test_hash_k_hybrid_matches_per_lane(hc):
-    """The latency kernels hash with pv_hash_k_hybrid (block words wave-uniform: the message schedule
-    on the scalar unit, the rounds on the vector unit); it, the per-lane pv_hash_k and hashlib agree
-    at every message length around the SHA-512 block and padding boundaries (libsodium's
-    SHA-512(R || A || M) reduced mod L)."""
-    import hashlib
-    rng = random.Random(31)
-    out = (ctypes.c_uint8 * 32)()
-    for mlen in list(range(0, 300)) + [rng.randrange(300, 5000) for _ in range(40)]:
-        sm = bytes(rng.getrandbits(8) for _ in range(64 + mlen))
-        pk = bytes(rng.getrandbits(8) for _ in range(32))
-        want = int.from_bytes(hashlib.sha512(sm[:32] + pk + sm[64:]).digest(), "little") % L
-        for hybrid in (0, 1):
-            hc.hc_hash_k(out, sm, ctypes.c_uint64(len(sm)), pk, hybrid)
-            assert int.from_bytes(bytes(out), "little") == want, (mlen, hybrid)
-

@@ -36,7 +36,7 @@ def main():
         buf = (ctypes.c_ulonglong * 16)()
         assert L.pv_debug_lat_trace(buf) == 0
         t = list(buf)
-        runs.append({i: round((t[i] - t[0]) / 100.0, 2) for i in (0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14)})
+        runs.append({i: round((t[i] - t[0]) / 100.0, 2) for i in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)})
         stats = {"lehmer_blocks": t[15] & 255, "block_quotients": (t[15] >> 8) & 255, "exact_steps": t[15] >> 16}
     med = {i: float(np.median([r[i] for r in runs])) for i in runs[0]}
     print(json.dumps({"lib": os.environ.get("PLENUM_AMD_LIB", "default"), "ok": bool(got[0]),
