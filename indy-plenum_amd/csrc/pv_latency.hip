@@ -264,9 +264,10 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 // window PV_LAT4_SPLIT (2^68), k_i = lo + 2^68 hi, so four waves run ~17 windows each at the same time:
 //   wave 0  decompression of A and R (one chain), -A and R' published (LDS flag), tables of -A and R';
 //           then lo(k1) on -A
-//   wave 1  checks, k, the split, s2 = k2 S mod L and its comb entries; then lo(k2) on -R' + [s2]B
-//   wave 2  waits for -A, doubles it 68 times, table of [2^68](-A); then hi(k1) on it
-//   wave 3  the same for R': table of [2^68]R'; then hi(k2) on its negation
+//   wave 1  checks, k, the split, s2 = k2 S mod L and its digits; then lo(k2) on -R'
+//   wave 2  [2^68](-A) by 68 doublings on y alone from A's encoding (lp_ydbl_chain), x once -A is
+//           published, table of it; then hi(k1) on it + positions 0..7 of [s2]B
+//   wave 3  the same for R': table of [2^68]R'; then hi(k2) on its negation + positions 8..15
 //   wave 0  sums the four parts, + R', compares with R' (lp_final_check).
 // A cached key keeps the two-wave cached flow (waves 2 and 3 only join the barriers).
 #ifndef PV_LAT4_MAX
@@ -301,6 +302,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
     __shared__ volatile uint32_t s_pts_ready;  // wave 0 -> waves 2, 3: -A and R' published
     __shared__ uint32_t s_pa[64], s_pr[64];    // -A, R' (ext)
     __shared__ uint32_t s_part[3][64];         // wave 1, 2, 3 results (ext)
+    __shared__ uint32_t s_fs[8];               // radix-65536 digits of s2 = k2 S mod L (waves 2, 3: [s2]B)
     __shared__ uint32_t s_tab[4][17][64];      // [j] of -A, R', [2^68](-A), [2^68]R', j = -8..8
     __shared__ uint32_t s_msg[ZC ? PV_ZC_MSG_WORDS : 1];
 
@@ -364,8 +366,20 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
             const int nw = __builtin_amdgcn_readfirstlane((int)s_nw);
             const int sgn = wave == 3 ? -1 : (s_neg ? -1 : 1);  // k2's part goes on -R''
             const uint32_t* dg = wave == 2 ? s_k1 : s_k2;
-            s_part[wave - 1][lane] = lp_straus_range(c, PV_LAT4_SPLIT, nw, [&](int i) { return sgn * pv_nibble(dg[i >> 3], i); },
-                                                     [&](int e) -> lu { return s_tab[wave][e + 8][lane]; });
+            // [s2]B in two halves: wave 2 positions 0..7, wave 3 8..15 of the fixed-base comb, the
+            // entries fetched before the loop and added after it (balances wave 1's lo(k2) loop)
+            const int j0 = wave == 2 ? 0 : PV_BCOMB_POS / 2;
+            uint32_t fsl[PV_BCOMB_POS / 4];
+#pragma unroll
+            for (int q = 0; q < PV_BCOMB_POS / 4; q++) fsl[q] = s_fs[j0 / 2 + q];
+            lu ent[PV_BCOMB_POS / 2];
+#pragma unroll
+            for (int jj = 0; jj < PV_BCOMB_POS / 2; jj++) ent[jj] = lp_bcomb_entry(c, bcomb, j0 + jj, pv_half(fsl[jj >> 1], jj));
+            lu acc = lp_straus_range(c, PV_LAT4_SPLIT, nw, [&](int i) { return sgn * pv_nibble(dg[i >> 3], i); },
+                                     [&](int e) -> lu { return s_tab[wave][e + 8][lane]; });
+#pragma unroll
+            for (int jj = PV_BCOMB_POS / 2 - 1; jj >= 0; jj--) acc = lp_add_cached(c, acc, lp_bcomb_fix(c, ent[jj], pv_half(fsl[jj >> 1], jj)));
+            s_part[wave - 1][lane] = acc;
         }
         __syncthreads();  // 2
         return;
@@ -405,9 +419,6 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
         uint32_t s2[8], fs[8], e1[8], e2[8];
         sc_mul(s2, hk.k2, S);
         sc_recode65536(fs, s2);
-        lu ent[PV_BCOMB_POS];
-#pragma unroll
-        for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
         sc_recode16(e1, hk.k1);
         sc_recode16(e2, hk.k2);
         const int nw1 = sc_nwin16(e1), nw2 = sc_nwin16(e2);
@@ -417,6 +428,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
             for (int q = 0; q < 8; q++) {
                 s_k1[q] = e1[q];
                 s_k2[q] = e2[q];
+                s_fs[q] = fs[q];
             }
             s_nw = (uint32_t)nw;
             s_neg = hk.neg ? 1u : 0u;
@@ -425,11 +437,8 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
         LAT_STAMP(10);
         __syncthreads();  // 1
         const int hi = nw < PV_LAT4_SPLIT ? nw : PV_LAT4_SPLIT;
-        lu acc = lp_straus_range(c, 0, hi, [&](int i) { return -pv_nibble(e2[i >> 3], i); },
-                                 [&](int e) -> lu { return s_tab[1][e + 8][lane]; });
-#pragma unroll
-        for (int j = PV_BCOMB_POS - 1; j >= 0; j--) acc = lp_add_cached(c, acc, lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)));
-        s_part[0][lane] = acc;
+        s_part[0][lane] = lp_straus_range(c, 0, hi, [&](int i) { return -pv_nibble(e2[i >> 3], i); },
+                                          [&](int e) -> lu { return s_tab[1][e + 8][lane]; });
         LAT_STAMP(11);
         __syncthreads();  // 2
         return;
@@ -478,12 +487,13 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
         LAT_STAMP(4);
         __syncthreads();  // 2
         LAT_STAMP(5);
-        // + the hi parts of k1 and k2 (waves 2, 3); wave 1's part is added by lp_final_check
+        // + the hi parts of k1 and k2 with the two halves of [s2]B (waves 2, 3); wave 1's part is added
+        // by lp_final_check
         QA = lp_add_cached(c, QA, lp_to_cached(c, lu(s_part[1][lane]), K.d2));
         QA = lp_add_cached(c, QA, lp_to_cached(c, lu(s_part[2][lane]), K.d2));
     }
-    // cached: QA = [k](-A), wave 1's part [S]B; otherwise QA = [k1](+-A) + R' + [2^68 hi(k2)](-R'), wave
-    // 1's part [lo(k2)](-R') + [s2]B
+    // cached: QA = [k](-A), wave 1's part [S]B; otherwise QA = [k1](+-A) + R' + [2^68 hi(k2)](-R') +
+    // [s2]B, wave 1's part [lo(k2)](-R')
     const bool eq = lp_final_check(c, K, QA, s_part[0][lane], dec.X, dec.Y);
     const bool ok = eq && key_ok && r_ok && s_sig_ok != 0;
     if constexpr (ZC) {
