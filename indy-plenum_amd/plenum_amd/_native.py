@@ -152,24 +152,58 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+_U8, _U64 = np.dtype(np.uint8), np.dtype(np.uint64)
+_fast = None  # the CPython binding (_fastcall) once bound to the loaded library, False if not built
+
+
+def _fastcall():
+    global _fast
+    if _fast is None:
+        if os.environ.get("PLENUM_AMD_NO_FASTCALL"):  # the ctypes path (A/B, debugging)
+            _fast = False
+            return _fast
+        try:
+            from . import _fastcall as fc
+            fc.bind(ctypes.cast(lib().pv_verify_batch, ctypes.c_void_p).value)
+            _fast = fc
+        except ImportError:
+            _fast = False
+    return _fast
+
+
+def _contig(a, dt):
+    if type(a) is np.ndarray and a.dtype == dt and a.flags.c_contiguous:
+        return a
+    return np.ascontiguousarray(a, dtype=dt)
+
+
 def verify_sm_batch(blob, offsets, pks):
     """crypto_sign_open verdicts for n concatenated (sig || msg) records.
 
     blob: uint8 array; offsets: uint64 array of n+1 prefix offsets into blob; pks: uint8 (n, 32).
     Returns a bool array of n verdicts (True = libnacl.crypto_sign_open would not raise)."""
-    ensure_device()
-    L = lib()
-    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-    n = len(offsets) - 1
+    if _device is None:
+        ensure_device()
+    offsets = _contig(offsets, _U64)
+    n = offsets.shape[0] - 1
     if n <= 0:
         return np.zeros(0, dtype=bool)
-    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    blob = _contig(blob, _U8)
     if blob.size == 0:
         blob = np.zeros(1, dtype=np.uint8)
-    pks = np.ascontiguousarray(pks, dtype=np.uint8).reshape(n, 32)
+    pks = _contig(pks, _U8)
+    if pks.size != 32 * n:
+        raise ValueError("pks must hold n x 32 key bytes")
     bits = np.zeros((n + 7) // 8, dtype=np.uint8)
-    check(L.pv_verify_batch(_ptr(blob), _ptr(offsets), n, _ptr(pks), _ptr(bits)), "pv_verify_batch")
-    return np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+    fc = _fast if _fast is not None else _fastcall()
+    if fc:  # the same C ABI call without ctypes' per-array marshalling (Plenum's small calls)
+        rc = fc.verify(blob, offsets, pks, bits)
+    else:
+        if int(offsets[n]) > blob.size:
+            raise ValueError("verify: inconsistent blob / offsets / keys / verdict sizes")
+        rc = lib().pv_verify_batch(_ptr(blob), _ptr(offsets), n, _ptr(pks), _ptr(bits))
+    check(rc, "pv_verify_batch")
+    return np.unpackbits(bits, count=n, bitorder="little").view(bool)
 
 
 def comb_fused():

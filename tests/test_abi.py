@@ -52,6 +52,30 @@ def test_no_gpu_fails_loudly(native):
         Verifier(bytes(32)).verify(bytes(64), b"msg")
 
 
+def test_fastcall_binding_matches_ctypes_entry(native):
+    """The CPython binding (plenum_amd/_fastcall.c: buffer protocol, GIL released) calls the same
+    pv_verify_batch the ctypes path binds: without an initialised device both return the library's
+    not-initialised code; inconsistent sizes are refused before the call."""
+    fc = native._fastcall()
+    if not fc:
+        pytest.skip("_fastcall not built (make -C indy-plenum_amd)")
+    L = native.lib()
+    if L.pv_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    blob, off = np.zeros(64, np.uint8), np.array([0, 64], np.uint64)
+    pks, bits = np.zeros((1, 32), np.uint8), np.zeros(1, np.uint8)
+    rc_c = L.pv_verify_batch(native._ptr(blob), native._ptr(off), 1, native._ptr(pks), native._ptr(bits))
+    assert rc_c != native.PV_OK and fc.verify(blob, off, pks, bits) == rc_c
+    for bad in ((blob, np.array([0, 65], np.uint64), pks, bits),           # record past the blob
+                (blob, off, np.zeros(16, np.uint8), bits),                  # short key array
+                (blob, np.array([0], np.uint64), pks, bits),                # no request
+                (blob, off, pks, np.zeros(0, np.uint8))):                   # no verdict byte
+        with pytest.raises(ValueError):
+            fc.verify(*bad)
+    with pytest.raises((TypeError, BufferError)):
+        fc.verify(blob, off, pks, bytes(1))                                 # read-only verdict buffer
+
+
 def test_b58decode_batch_vs_restatement():
     from plenum_amd.base58 import b58decode_many, b58encode
     rng = random.Random(4)
