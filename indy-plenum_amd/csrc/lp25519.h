@@ -758,8 +758,9 @@ LP_FN lu lp_comb_a(const LpLane& c, const Entry& entry) {
 // Y row 1 = y_R), and x_R != 0 or sign 0; accept iff X_Q = x_R Z_Q and Y_Q = y_R Z_Q. Given y_Q =
 // y_R, the two roots x, -x have opposite parity (p odd) unless x = 0, so parity(x_Q) = sign(R)
 // exactly when x_Q is the root decompression picked; y_Q = y_R < p is the canonical-y condition.
-LP_FN bool lp_final_check(const LpLane& c, const LpConsts& K, const lu& QA, const lu& SB, const lu& X, const lu& Y) {
-    const lu sb = lp_to_cached(c, SB, K.d2);
+// sb: the second summand already in cached form (the four-wave kernel's waves convert their parts
+// before the last barrier, off wave 0's chain).
+LP_FN bool lp_final_check_cached(const LpLane& c, const lu& QA, const lu& sb, const lu& X, const lu& Y) {
     const lu Q = lp_add_cached(c, QA, sb);
     lu QX, QY, QZ, QT;
     lp_allrows(Q, QX, QY, QZ, QT);
@@ -770,6 +771,9 @@ LP_FN bool lp_final_check(const LpLane& c, const LpConsts& K, const lu& QA, cons
     const lu prod = lp_mul(c, c.rows(xr[1], yr[1], 0u, 0u), QZ);
     const lu diff = lp_sub(c, c.rows(QX, QY, 0u, 0u), prod);
     return lp_row_iszero(diff, 0) && lp_row_iszero(diff, 1);
+}
+LP_FN bool lp_final_check(const LpLane& c, const LpConsts& K, const lu& QA, const lu& SB, const lu& X, const lu& Y) {
+    return lp_final_check_cached(c, QA, lp_to_cached(c, SB, K.d2), X, Y);
 }
 
 // ------------------------------------------------------------------ the half-size split, limb-parallel

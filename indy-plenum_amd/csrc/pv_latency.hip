@@ -301,7 +301,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
     __shared__ uint32_t s_sig_ok, s_nw, s_neg;
     __shared__ volatile uint32_t s_pts_ready;  // wave 0 -> waves 2, 3: -A and R' published
     __shared__ uint32_t s_pa[64], s_pr[64];    // -A, R' (ext)
-    __shared__ uint32_t s_part[3][64];         // wave 1, 2, 3 results (ext)
+    __shared__ uint32_t s_part[3][64];         // wave 1, 2, 3 results (cached form)
     __shared__ uint32_t s_fs[8];               // radix-65536 digits of s2 = k2 S mod L (waves 2, 3: [s2]B)
     __shared__ uint32_t s_tab[4][17][64];      // [j] of -A, R', [2^68](-A), [2^68]R', j = -8..8
     __shared__ uint32_t s_msg[ZC ? PV_ZC_MSG_WORDS : 1];
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
                                      [&](int e) -> lu { return s_tab[wave][e + 8][lane]; });
 #pragma unroll
             for (int jj = PV_BCOMB_POS / 2 - 1; jj >= 0; jj--) acc = lp_add_cached(c, acc, lp_bcomb_fix(c, ent[jj], pv_half(fsl[jj >> 1], jj)));
-            s_part[wave - 1][lane] = acc;
+            s_part[wave - 1][lane] = lp_to_cached(c, acc, K.d2);  // cached here, off wave 0's chain
         }
         __syncthreads();  // 2
         return;
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
                 s_sig_ok = sig_ok ? 1u : 0u;
             }
             __syncthreads();  // 1
-            s_part[0][lane] = lp_comb_b(c, [&](int j) -> lu { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); });
+            s_part[0][lane] = lp_to_cached(c, lp_comb_b(c, [&](int j) -> lu { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); }), K.d2);
             __syncthreads();  // 2
             return;
         }
@@ -437,8 +437,8 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
         LAT_STAMP(10);
         __syncthreads();  // 1
         const int hi = nw < PV_LAT4_SPLIT ? nw : PV_LAT4_SPLIT;
-        s_part[0][lane] = lp_straus_range(c, 0, hi, [&](int i) { return -pv_nibble(e2[i >> 3], i); },
-                                          [&](int e) -> lu { return s_tab[1][e + 8][lane]; });
+        s_part[0][lane] = lp_to_cached(c, lp_straus_range(c, 0, hi, [&](int i) { return -pv_nibble(e2[i >> 3], i); },
+                                                          [&](int e) -> lu { return s_tab[1][e + 8][lane]; }), K.d2);
         LAT_STAMP(11);
         __syncthreads();  // 2
         return;
@@ -489,12 +489,12 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
         LAT_STAMP(5);
         // + the hi parts of k1 and k2 with the two halves of [s2]B (waves 2, 3); wave 1's part is added
         // by lp_final_check
-        QA = lp_add_cached(c, QA, lp_to_cached(c, lu(s_part[1][lane]), K.d2));
-        QA = lp_add_cached(c, QA, lp_to_cached(c, lu(s_part[2][lane]), K.d2));
+        QA = lp_add_cached(c, QA, lu(s_part[1][lane]));
+        QA = lp_add_cached(c, QA, lu(s_part[2][lane]));
     }
     // cached: QA = [k](-A), wave 1's part [S]B; otherwise QA = [k1](+-A) + R' + [2^68 hi(k2)](-R') +
     // [s2]B, wave 1's part [lo(k2)](-R')
-    const bool eq = lp_final_check(c, K, QA, s_part[0][lane], dec.X, dec.Y);
+    const bool eq = lp_final_check_cached(c, QA, s_part[0][lane], dec.X, dec.Y);
     const bool ok = eq && key_ok && r_ok && s_sig_ok != 0;
     if constexpr (ZC) {
         // a coherent (fine-grained) pinned byte the host spins on while the kernel runs

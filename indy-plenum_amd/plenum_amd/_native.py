@@ -171,12 +171,6 @@ def _fastcall():
     return _fast
 
 
-def _contig(a, dt):
-    if type(a) is np.ndarray and a.dtype == dt and a.flags.c_contiguous:
-        return a
-    return np.ascontiguousarray(a, dtype=dt)
-
-
 def verify_sm_batch(blob, offsets, pks):
     """crypto_sign_open verdicts for n concatenated (sig || msg) records.
 
@@ -184,25 +178,31 @@ def verify_sm_batch(blob, offsets, pks):
     Returns a bool array of n verdicts (True = libnacl.crypto_sign_open would not raise)."""
     if _device is None:
         ensure_device()
-    offsets = _contig(offsets, _U64)
+    # numpy inputs of the right type and layout pass through untouched (Plenum's small calls: every
+    # microsecond here is on the request's latency)
+    if type(offsets) is not np.ndarray or offsets.dtype != _U64 or not offsets.flags.c_contiguous:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     n = offsets.shape[0] - 1
     if n <= 0:
         return np.zeros(0, dtype=bool)
-    blob = _contig(blob, _U8)
+    if type(blob) is not np.ndarray or blob.dtype != _U8 or not blob.flags.c_contiguous:
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
     if blob.size == 0:
         blob = np.zeros(1, dtype=np.uint8)
-    pks = _contig(pks, _U8)
+    if type(pks) is not np.ndarray or pks.dtype != _U8 or not pks.flags.c_contiguous:
+        pks = np.ascontiguousarray(pks, dtype=np.uint8)
     if pks.size != 32 * n:
         raise ValueError("pks must hold n x 32 key bytes")
     bits = np.zeros((n + 7) // 8, dtype=np.uint8)
     fc = _fast if _fast is not None else _fastcall()
-    if fc:  # the same C ABI call without ctypes' per-array marshalling (Plenum's small calls)
+    if fc:  # the same C ABI call without ctypes' per-array marshalling
         rc = fc.verify(blob, offsets, pks, bits)
     else:
         if int(offsets[n]) > blob.size:
             raise ValueError("verify: inconsistent blob / offsets / keys / verdict sizes")
         rc = lib().pv_verify_batch(_ptr(blob), _ptr(offsets), n, _ptr(pks), _ptr(bits))
-    check(rc, "pv_verify_batch")
+    if rc:
+        check(rc, "pv_verify_batch")
     return np.unpackbits(bits, count=n, bitorder="little").view(bool)
 
 
