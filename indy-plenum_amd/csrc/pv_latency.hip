@@ -43,7 +43,7 @@
 // PV_LAT_TRACE (measurement builds only): block 0 stamps s_memrealtime (100 MHz) at its phase
 // boundaries into pv_lat_trace, read back by pv_debug_lat_trace.
 #ifdef PV_LAT_TRACE
-__device__ unsigned long long pv_lat_trace_buf[16];
+__device__ unsigned long long pv_lat_trace_buf[20];
 #define LAT_STAMP(i) do { if (blockIdx.x == 0 && (threadIdx.x & 63u) == 0) pv_lat_trace_buf[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define LAT_STAMP(i) do { } while (0)
@@ -307,6 +307,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
     __shared__ uint32_t s_msg[ZC ? PV_ZC_MSG_WORDS : 1];
 
     if (threadIdx.x == 0) s_pts_ready = 0u;
+    LAT_STAMP(wave == 0 ? 16 : 19);  // kernel entry (19: unused slot for the other waves)
     uint64_t smlen;
     const uint32_t* ap;
     uint32_t sh;
@@ -315,6 +316,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
         const uint32_t* src = reinterpret_cast<const uint32_t*>(sm + (uint64_t)r * zstride);
         for (uint32_t t = threadIdx.x; t < zstride / 4; t += LAT4_THREADS) s_msg[t] = src[t];
         __syncthreads();
+        LAT_STAMP(wave == 0 ? 17 : 19);  // the slot is in LDS
         smlen = s_msg[0];
 #pragma unroll
         for (int q = 0; q < 8; q++) in.A[q] = s_msg[PV_ZC_PK_WORD + q];
