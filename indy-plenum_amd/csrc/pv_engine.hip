@@ -3171,9 +3171,9 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
             uint8_t* vb = g_ctx.h_zc_verdict;  // coherent pinned memory, read while the kernel runs
             uint8_t* slots = g_ctx.h_stage;
             memset(vb, 0xFF, n);  // pending (PV_ZC_SPIN)
-            auto fill = [&](uint64_t a, uint64_t b) {
+            auto fill_at = [&](uint8_t* base, uint64_t a, uint64_t b) {
                 for (uint64_t i = a; i < b; i++) {
-                    uint8_t* sl = slots + i * stride;
+                    uint8_t* sl = base + i * stride;
                     const uint64_t len = sm_off[i + 1] - sm_off[i];
                     const uint32_t hdr[PV_ZC_PK_WORD] = {(uint32_t)len, 0u, 0u, 0u};
                     memcpy(sl, hdr, sizeof(hdr));
@@ -3182,11 +3182,15 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
                     memset(sl + 4 * PV_ZC_REC_WORD + len, 0, stride - 4 * PV_ZC_REC_WORD - len);
                 }
             };
-            if (n * stride < (128u << 10)) {
-                fill(0, n);
+            const bool one = n == 1 && stride <= sizeof(PvZcOne);  // the slot goes in the kernel arguments
+            PvZcOne one_slot;
+            if (one) {
+                fill_at(reinterpret_cast<uint8_t*>(one_slot.w), 0, 1);
+            } else if (n * stride < (128u << 10)) {
+                fill_at(slots, 0, n);
             } else {  // node-quota sizes: the slots are written by the copy pool's threads
                 const unsigned k = 8;
-                g_copy_pool.run(k, [&](unsigned t) { fill(n * t / k, n * (t + 1) / k); });
+                g_copy_pool.run(k, [&](unsigned t) { fill_at(slots, n * t / k, n * (t + 1) / k); });
             }
             hipStream_t s = g_ctx.stream;
             if (g_ctx.last_stream && g_ctx.last_stream != s)
@@ -3195,7 +3199,8 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
             g_ctx.last_keyed = false;
             g_ctx.last_dev_choice = false;
             g_ctx.last_zero_copy = true;
-            rc = pv_latency_launch_zc(slots, (uint32_t)stride, n, g_ctx.d_bcomb, kc_view(), vb, s);
+            rc = one ? pv_latency_launch_zc_one(one_slot, (uint32_t)stride, g_ctx.d_bcomb, kc_view(), vb, s)
+                     : pv_latency_launch_zc(slots, (uint32_t)stride, n, g_ctx.d_bcomb, kc_view(), vb, s);
             PV_HIP(hipEventRecord(g_ctx.ev_launch_done, s), PV_ERR_LAUNCH);
             g_ctx.last_stream = s;
             if (rc) {

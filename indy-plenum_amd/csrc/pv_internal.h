@@ -32,5 +32,12 @@ int pv_latency_launch_zc(const uint8_t* h_slots, uint32_t stride, uint64_t n, co
 static constexpr uint64_t PV_ZC_MAX_REQ = 2048;
 static constexpr uint32_t PV_ZC_MAX_STRIDE = 2048;  // bytes per slot (the LDS copy)
 static constexpr uint32_t PV_ZC_PK_WORD = 4, PV_ZC_REC_WORD = 12, PV_ZC_SLACK = 160;
+// A one-request zero-copy call whose slot (same layout) fits PvZcOne travels in the kernel arguments
+// (pv_latency_launch_zc_one): records up to 1,024 - 48 - 160 = 816 bytes.
+struct PvZcOne {
+    uint32_t w[256];
+};
+int pv_latency_launch_zc_one(const PvZcOne& one, uint32_t stride, const void* d_bcomb, const PvKeyCacheView& kc,
+                             uint8_t* h_vbytes, hipStream_t stream);
 
 #endif  // PV_INTERNAL_H

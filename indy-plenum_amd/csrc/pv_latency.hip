@@ -283,14 +283,15 @@ constexpr int LAT4_THREADS = 256;
 // one byte per request stored to host memory (vbytes) instead of OR-ed into device words: no copy
 // kernels before or after the verification.
 
+// The four-wave body; zsrc (ZC): this workgroup's request slot, in pinned host memory
+// (pv_lat4_kernel) or in the kernel arguments (pv_lat4_one_kernel).
 template <bool ZC>
-__global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __restrict__ sm,
-                                                               const uint64_t* __restrict__ off, uint64_t n,
-                                                               const uint8_t* __restrict__ pk,
-                                                               const uint32_t* __restrict__ bcomb, PvKeyCacheView kc,
-                                                               unsigned long long* __restrict__ verdict,
-                                                               uint8_t* __restrict__ vbytes, uint32_t zstride,
-                                                               const uint32_t* __restrict__ run_if) {
+__device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, const uint8_t* __restrict__ sm,
+                                          const uint64_t* __restrict__ off, uint64_t n,
+                                          const uint8_t* __restrict__ pk, const uint32_t* __restrict__ bcomb,
+                                          PvKeyCacheView kc, unsigned long long* __restrict__ verdict,
+                                          uint8_t* __restrict__ vbytes, uint32_t zstride,
+                                          const uint32_t* __restrict__ run_if) {
 #if LP_DEVICE
     if (run_if && *run_if == 0u) return;
     const uint32_t r = blockIdx.x;
@@ -313,8 +314,7 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
     uint32_t sh;
     pv_sig_words in;
     if constexpr (ZC) {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(sm + (uint64_t)r * zstride);
-        for (uint32_t t = threadIdx.x; t < zstride / 4; t += LAT4_THREADS) s_msg[t] = src[t];
+        for (uint32_t t = threadIdx.x; t < zstride / 4; t += LAT4_THREADS) s_msg[t] = zsrc[t];
         __syncthreads();
         LAT_STAMP(wave == 0 ? 17 : 19);  // the slot is in LDS
         smlen = s_msg[0];
@@ -511,6 +511,27 @@ __global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __
 #endif
 }
 
+template <bool ZC>
+__global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_kernel(const uint8_t* __restrict__ sm,
+                                                               const uint64_t* __restrict__ off, uint64_t n,
+                                                               const uint8_t* __restrict__ pk,
+                                                               const uint32_t* __restrict__ bcomb, PvKeyCacheView kc,
+                                                               unsigned long long* __restrict__ verdict,
+                                                               uint8_t* __restrict__ vbytes, uint32_t zstride,
+                                                               const uint32_t* __restrict__ run_if) {
+    lat4_body<ZC>(ZC ? reinterpret_cast<const uint32_t*>(sm + (uint64_t)blockIdx.x * zstride) : nullptr, sm, off, n,
+                  pk, bcomb, kc, verdict, vbytes, zstride, run_if);
+}
+
+// One request whose slot travels in the kernel arguments (pv_latency_launch_zc_one): the runtime
+// writes them next to the dispatch, so the slot is read from there at the kernel's start instead of
+// from pinned host memory over PCIe.
+__global__ __launch_bounds__(LAT4_THREADS) void pv_lat4_one_kernel(PvZcOne one, const uint32_t* __restrict__ bcomb,
+                                                                   PvKeyCacheView kc, uint8_t* __restrict__ vbytes,
+                                                                   uint32_t zstride) {
+    lat4_body<true>(one.w, nullptr, nullptr, 1, nullptr, bcomb, kc, nullptr, vbytes, zstride, nullptr);
+}
+
 }  // namespace
 
 #ifdef PV_LAT_TRACE
@@ -540,6 +561,16 @@ int pv_latency_launch(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, co
                            reinterpret_cast<unsigned long long*>(d_verdict), nullptr, 0u, run_if);
     e = hipGetLastError();
     if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("pv_lat_kernel: ") + hipGetErrorString(e));
+    return PV_OK;
+}
+
+int pv_latency_launch_zc_one(const PvZcOne& one, uint32_t stride, const void* d_bcomb, const PvKeyCacheView& kc,
+                             uint8_t* h_vbytes, hipStream_t stream) {
+    if (stride % 64 || stride > sizeof(PvZcOne)) return pv_fail(PV_ERR_ARG, "pv_latency_launch_zc_one: bad slot size");
+    hipLaunchKernelGGL(pv_lat4_one_kernel, dim3(1), dim3(LAT4_THREADS), 0, stream, one,
+                       reinterpret_cast<const uint32_t*>(d_bcomb), kc, h_vbytes, stride);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return pv_fail(PV_ERR_LAUNCH, std::string("pv_lat4_one_kernel: ") + hipGetErrorString(e));
     return PV_OK;
 }
 

@@ -137,6 +137,24 @@ def test_small_calls_zero_copy_records(native, sodium, oracle):
         assert native.last_zero_copy() == (native.last_path()[0] == native.PV_PATH_LATENCY), lead
 
 
+def test_one_request_calls(native, sodium, oracle):
+    """One-request host-buffer calls (verifySignature singletons): a slot of <= 1,024 bytes (records
+    up to 816 bytes) travels in the kernel arguments (pv_lat4_one_kernel), longer ones in a pinned
+    slot; valid and tampered records on both sides of that edge, every alignment, each call alone."""
+    lengths = [0, 1, 127, 128, 300, 700, 744, 748, 752, 756, 760, 800]
+    cases = _long_record_cases(sodium, oracle, lengths, seed=18)
+    want = reference_verdicts(sodium, cases)
+    assert want.sum() == len(cases) // 2
+    assert any(len(sm) <= 816 for sm, _ in cases) and any(len(sm) > 816 for sm, _ in cases)
+    for i, (sm, pk) in enumerate(cases):
+        blob, off, pks = pack([(sm, pk)])
+        for lead in (0, 1, 2, 3):
+            blob2 = np.concatenate([np.full(lead, 0x55, np.uint8), blob])
+            got = native.verify_sm_batch(blob2, off + lead, pks)
+            assert bool(got[0]) == bool(want[i]), (len(sm), lead)
+            assert native.last_zero_copy() == (native.last_path()[0] == native.PV_PATH_LATENCY), (len(sm), lead)
+
+
 def test_small_calls_long_records(native, sodium, oracle):
     """Small host-buffer calls with records beyond a zero-copy slot (1,841 bytes up to 9 KB): the
     whole call takes the staged copy form (the zero-copy choice is made per call from the longest
