@@ -611,6 +611,35 @@ LP_FN void lp_build_a_table(const LpLane& c, const LpConsts& K, const lu& negA, 
     }
 }
 
+// One half of that table, for two waves building it at once: part 0 the entries 0, +-1..+-4 (one
+// doubling, two additions), part 1 the entries +-5..+-8 from [4]P = 2(2P) (two doublings, four
+// additions). Same points as lp_build_a_table (any projective representative serves a lookup).
+template <class Store>
+LP_FN void lp_build_a_table_part(const LpLane& c, const LpConsts& K, const lu& P, int part, const Store& store) {
+    const lu c1 = lp_to_cached(c, P, K.d2);
+    if (part == 0) {
+        const lu one = K.one, two = lp_sel(c.k0, 2u, 0u);
+        store(0, c.rows(one, one, 0u, two));
+        store(1, c1);
+        store(-1, lp_neg_cached(c, c1));
+        lu cur = lp_dbl(c, P);
+        for (int j = 2; j <= 4; j++) {
+            if (j > 2) cur = lp_add_cached(c, cur, c1);
+            const lu cj = lp_to_cached(c, cur, K.d2);
+            store(j, cj);
+            store(-j, lp_neg_cached(c, cj));
+        }
+        return;
+    }
+    lu cur = lp_dbl(c, lp_dbl(c, P));  // [4]P
+    for (int j = 5; j <= 8; j++) {
+        cur = lp_add_cached(c, cur, c1);
+        const lu cj = lp_to_cached(c, cur, K.d2);
+        store(j, cj);
+        store(-j, lp_neg_cached(c, cj));
+    }
+}
+
 // [2^n] P without P's x: on -x^2 + y^2 = 1 + d x^2 y^2, x^2 = (y^2 - 1) / (d y^2 + 1) is a function of
 // y, so doubling maps y to a function of y alone, and x to x times a function of y:
 //   y' = (d a^2 + 2ab - b^2) / (-d a^2 + 2d ab + b^2),  x' / x = 2YZ (d a + b) / (d a^2 + b^2)

@@ -65,6 +65,32 @@ struct LatMsg {
 
 [[maybe_unused]] constexpr uint32_t PV_ZC_MSG_WORDS = PV_ZC_MAX_STRIDE / 4;
 
+// PV_LAT_SHA_CALL = 1: the four-wave form's SHA-512 (wave 1) is a real call with its own register
+// allocation, so its speed does not move with the code around it (inlined, one request's hash took
+// 24.0-26.4 us depending on the rest of the kernel); 0: inlined. The two-wave form keeps it inlined
+// (a call raises every caller's VGPR count to the callee's, and that form runs several workgroups
+// per CU).
+#ifndef PV_LAT_SHA_CALL
+#define PV_LAT_SHA_CALL 1
+#endif
+struct LatK {
+    uint32_t k[8];
+};
+__device__ __noinline__ LatK lat_hash_k_call(pv_sig_words in, uint64_t smlen, const uint32_t* ap, uint32_t sh) {
+    LatK o;
+    pv_hash_k(o.k, in, smlen, LatMsg{ap, sh});
+    return o;
+}
+__device__ __forceinline__ void lat_hash_k(uint32_t k[8], const pv_sig_words& in, uint64_t smlen, const LatMsg& mw) {
+#if PV_LAT_SHA_CALL
+    const LatK o = lat_hash_k_call(in, smlen, mw.ap, mw.sh);
+#pragma unroll
+    for (int q = 0; q < 8; q++) k[q] = o.k[q];
+#else
+    pv_hash_k(k, in, smlen, mw);
+#endif
+}
+
 // ZC: zero-copy host-buffer call (pv_latency_launch_zc; slot layout and verdict bytes as in
 // pv_lat4_kernel below).
 template <bool ZC>
@@ -262,12 +288,13 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 
 // Four-wave form for small batches (PV_LAT4_MAX): each of [k1](+-A) and [k2](-R') is split once more at
 // window PV_LAT4_SPLIT (2^68), k_i = lo + 2^68 hi, so four waves run ~17 windows each at the same time:
-//   wave 0  decompression of A and R (one chain), -A and R' published (LDS flag), tables of -A and R';
+//   wave 0  decompression of A and R (one chain), -A and R' published (LDS flag), tables of -A and the lower half of R'
 //           then lo(k1) on -A
 //   wave 1  checks, k, the split, s2 = k2 S mod L and its digits; then lo(k2) on -R'
 //   wave 2  [2^68](-A) by 68 doublings on y alone from A's encoding (lp_ydbl_chain), x once -A is
 //           published, table of it; then hi(k1) on it + positions 0..7 of [s2]B
-//   wave 3  the same for R': table of [2^68]R'; then hi(k2) on its negation + positions 8..15
+//   wave 3  the same for R': table of [2^68]R' and the upper half of R''s table; then hi(k2) on its
+//           negation + positions 8..15
 //   wave 0  sums the four parts, + R', compares with R' (lp_final_check).
 // A cached key keeps the two-wave cached flow (waves 2 and 3 only join the barriers).
 #ifndef PV_LAT4_MAX
@@ -275,6 +302,10 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 #endif
 #ifndef PV_LAT4_SPLIT
 #define PV_LAT4_SPLIT 17
+#endif
+// PV_LAT4_RTAB_SPLIT = 1: R''s table is built half by wave 0 and half by wave 3; 0: all by wave 0
+#ifndef PV_LAT4_RTAB_SPLIT
+#define PV_LAT4_RTAB_SPLIT 1
 #endif
 constexpr int LAT4_THREADS = 256;
 // ZC (zero-copy host-buffer calls, pv_latency_launch_zc): the requests sit in pinned host memory in
@@ -362,6 +393,10 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
             lp_allrows(wave == 2 ? lu(s_pa[lane]) : lu(s_pr[lane]), x0, t1, t2, t3);  // ext rows [x, y, 1, xy]
             const lu P = lp_ydbl_finish(c, K, ch, x0);
             lp_build_a_table(c, K, P, [&](int j, const lu& q) { s_tab[wave][j + 8][lane] = q; });
+            // wave 3 also builds the upper half of R''s table (wave 0 the lower half): wave 0's
+            // decompression + tables were the longest chain before barrier 1
+            if (wave == 3 && PV_LAT4_RTAB_SPLIT)
+                lp_build_a_table_part(c, K, lu(s_pr[lane]), 1, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });
         }
         __syncthreads();  // 1: split, tables ready
         if (!cached) {
@@ -395,7 +430,7 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
 #pragma unroll
             for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb, j, pv_half(fs[j >> 1], j));
             uint32_t k[8], e256[8];
-            pv_hash_k(k, in, smlen, mw);
+            lat_hash_k(k, in, smlen, mw);
             sc_recode256(e256, k);
             if (lane == 0) {
 #pragma unroll
@@ -408,7 +443,7 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
             return;
         }
         uint32_t k[8], S[8];
-        pv_hash_k(k, in, smlen, mw);
+        lat_hash_k(k, in, smlen, mw);
         LAT_STAMP(9);
 #pragma unroll
         for (int q = 0; q < 8; q++) {
@@ -476,7 +511,10 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) s_pts_ready = 1u;
         lp_build_a_table(c, K, negA, [&](int j, const lu& q) { s_tab[0][j + 8][lane] = q; });
-        lp_build_a_table(c, K, Rp, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });
+        if (PV_LAT4_RTAB_SPLIT)
+            lp_build_a_table_part(c, K, Rp, 0, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });  // wave 3: part 1
+        else
+            lp_build_a_table(c, K, Rp, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });
         LAT_STAMP(2);
         __syncthreads();  // 1
         LAT_STAMP(3);
