@@ -611,32 +611,36 @@ LP_FN void lp_build_a_table(const LpLane& c, const LpConsts& K, const lu& negA, 
     }
 }
 
-// One half of that table, for two waves building it at once: part 0 the entries 0, +-1..+-4 (one
-// doubling, two additions), part 1 the entries +-5..+-8 from [4]P = 2(2P) (two doublings, four
-// additions). Same points as lp_build_a_table (any projective representative serves a lookup).
+// Parts of that table for waves building it at once: part 0 the entries 0, +-1..+-4 (one doubling,
+// two additions), part 1 +-5, +-6 from [4]P = 2(2P) (two doublings, two additions), part 2 +-7, +-8
+// from [8]P = 2(2(2P)) and [7]P = [8]P - P (three doublings, one addition). Same points as
+// lp_build_a_table (any projective representative serves a lookup).
 template <class Store>
 LP_FN void lp_build_a_table_part(const LpLane& c, const LpConsts& K, const lu& P, int part, const Store& store) {
     const lu c1 = lp_to_cached(c, P, K.d2);
+    auto put = [&](int j, const lu& pt) {
+        const lu cj = lp_to_cached(c, pt, K.d2);
+        store(j, cj);
+        store(-j, lp_neg_cached(c, cj));
+    };
     if (part == 0) {
         const lu one = K.one, two = lp_sel(c.k0, 2u, 0u);
         store(0, c.rows(one, one, 0u, two));
         store(1, c1);
         store(-1, lp_neg_cached(c, c1));
         lu cur = lp_dbl(c, P);
-        for (int j = 2; j <= 4; j++) {
-            if (j > 2) cur = lp_add_cached(c, cur, c1);
-            const lu cj = lp_to_cached(c, cur, K.d2);
-            store(j, cj);
-            store(-j, lp_neg_cached(c, cj));
-        }
-        return;
-    }
-    lu cur = lp_dbl(c, lp_dbl(c, P));  // [4]P
-    for (int j = 5; j <= 8; j++) {
+        put(2, cur);
         cur = lp_add_cached(c, cur, c1);
-        const lu cj = lp_to_cached(c, cur, K.d2);
-        store(j, cj);
-        store(-j, lp_neg_cached(c, cj));
+        put(3, cur);
+        put(4, lp_add_cached(c, cur, c1));
+    } else if (part == 1) {
+        lu cur = lp_add_cached(c, lp_dbl(c, lp_dbl(c, P)), c1);  // [5]P
+        put(5, cur);
+        put(6, lp_add_cached(c, cur, c1));
+    } else {
+        const lu p8 = lp_dbl(c, lp_dbl(c, lp_dbl(c, P)));
+        put(8, p8);
+        put(7, lp_add_cached(c, p8, lp_neg_cached(c, c1)));
     }
 }
 

@@ -293,8 +293,8 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 //   wave 1  checks, k, the split, s2 = k2 S mod L and its digits; then lo(k2) on -R'
 //   wave 2  [2^68](-A) by 68 doublings on y alone from A's encoding (lp_ydbl_chain), x once -A is
 //           published, table of it; then hi(k1) on it + positions 0..7 of [s2]B
-//   wave 3  the same for R': table of [2^68]R' and the upper half of R''s table; then hi(k2) on its
-//           negation + positions 8..15
+//   wave 3  the same for R': table of [2^68]R'; then hi(k2) on its negation + positions 8..15
+//   waves 2, 3 also build R''s table entries 5, 6 / 7, 8 (wave 0 entries 0..4)
 //   wave 0  sums the four parts, + R', compares with R' (lp_final_check).
 // A cached key keeps the two-wave cached flow (waves 2 and 3 only join the barriers).
 #ifndef PV_LAT4_MAX
@@ -303,7 +303,8 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 #ifndef PV_LAT4_SPLIT
 #define PV_LAT4_SPLIT 17
 #endif
-// PV_LAT4_RTAB_SPLIT = 1: R''s table is built half by wave 0 and half by wave 3; 0: all by wave 0
+// PV_LAT4_RTAB_SPLIT = 1: R''s table is built by waves 0 (entries 0..4), 2 (5, 6) and 3 (7, 8); 0: all
+// by wave 0
 #ifndef PV_LAT4_RTAB_SPLIT
 #define PV_LAT4_RTAB_SPLIT 1
 #endif
@@ -393,10 +394,10 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
             lp_allrows(wave == 2 ? lu(s_pa[lane]) : lu(s_pr[lane]), x0, t1, t2, t3);  // ext rows [x, y, 1, xy]
             const lu P = lp_ydbl_finish(c, K, ch, x0);
             lp_build_a_table(c, K, P, [&](int j, const lu& q) { s_tab[wave][j + 8][lane] = q; });
-            // wave 3 also builds the upper half of R''s table (wave 0 the lower half): wave 0's
-            // decompression + tables were the longest chain before barrier 1
-            if (wave == 3 && PV_LAT4_RTAB_SPLIT)
-                lp_build_a_table_part(c, K, lu(s_pr[lane]), 1, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });
+            // waves 2 and 3 also build the upper entries of R''s table (wave 0 the lower ones): wave
+            // 0's decompression + tables were the longest chain before barrier 1
+            if (PV_LAT4_RTAB_SPLIT)
+                lp_build_a_table_part(c, K, lu(s_pr[lane]), wave - 1, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });
         }
         __syncthreads();  // 1: split, tables ready
         if (!cached) {
@@ -512,7 +513,7 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
         if (lane == 0) s_pts_ready = 1u;
         lp_build_a_table(c, K, negA, [&](int j, const lu& q) { s_tab[0][j + 8][lane] = q; });
         if (PV_LAT4_RTAB_SPLIT)
-            lp_build_a_table_part(c, K, Rp, 0, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });  // wave 3: part 1
+            lp_build_a_table_part(c, K, Rp, 0, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });  // waves 2, 3: 5..8
         else
             lp_build_a_table(c, K, Rp, [&](int j, const lu& q) { s_tab[1][j + 8][lane] = q; });
         LAT_STAMP(2);

@@ -359,6 +359,32 @@ int hc_lp_ydbl_check(const uint8_t* a_enc, const uint8_t* r_enc, int n) {
     }
     return mask;
 }
+// lp_build_a_table_part (the four-wave kernel's R' table built by three waves): 1 if parts 0, 1, 2
+// together give the points of lp_build_a_table at every entry j = -8..8, 0 if not, -1 if the
+// encoding does not decompress.
+int hc_lp_table_parts_check(const uint8_t* enc) {
+    uint32_t wa[8];
+    load_words(wa, enc);
+    const LpLane c = LpLane::make();
+    const LpConsts K = LpConsts::make(c);
+    lu sw[8];
+    for (int q = 0; q < 8; q++) sw[q] = wa[q];
+    const LpDecomp d = lp_decompress_ar(c, K, sw);
+    if (!d.ok_a) return -1;
+    const lu P = lp_ext_from_xy(c, K, d.X, d.Y, 0);
+    lu full[17], part[17];
+    lp_build_a_table(c, K, P, [&](int j, const lu& q) { full[j + 8] = q; });
+    for (int pt = 0; pt < 3; pt++) lp_build_a_table_part(c, K, P, pt, [&](int j, const lu& q) { part[j + 8] = q; });
+    for (int e = 0; e < 17; e++)
+        for (int r = 0; r < 3; r++) {  // cached rows [Y-X, Y+X, 2dT] against 2Z (row 3)
+            fe a, b, dd;
+            fe_mul(a, lp_row_fe(full[e], r), lp_row_fe(part[e], 3));
+            fe_mul(b, lp_row_fe(part[e], r), lp_row_fe(full[e], 3));
+            fe_sub(dd, a, b);
+            if (!fe_iszero(dd)) return 0;
+        }
+    return 1;
+}
 // lp_halfsize's counts for one scalar: [0] Lehmer blocks, [1] quotients settled inside them, [2] exact steps
 void hc_lp_halfsize_stats(const uint8_t* k, uint32_t* stats) {
     uint32_t kw[8];

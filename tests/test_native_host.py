@@ -426,3 +426,19 @@ def test_lp_ydbl_chain_matches_doublings(hc):
             assert got == 3, (i, n)
             tested += 1
     assert tested >= 50
+
+
+def test_lp_table_parts_match_full_table(hc):
+    """The four-wave kernel builds R''s [j] table in three parts on three waves (entries 0..4 by one
+    doubling and additions, 5-6 from [4]P, 7-8 from [8]P and [8]P - P): every entry is the same point
+    as lp_build_a_table's."""
+    rng = random.Random(47)
+    tested = 0
+    for _ in range(300):
+        got = hc.hc_lp_table_parts_check(bytes(rng.getrandbits(8) for _ in range(32)))
+        if got == -1:
+            continue
+        assert got == 1
+        tested += 1
+    assert tested >= 50
+
