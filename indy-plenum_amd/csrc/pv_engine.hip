@@ -643,7 +643,7 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_split_kernel(const uint8_t* __res
         pv_halfk hk;
         sc_halfsize(hk, k);
         uint32_t s2[8];
-        sc_mul(s2, hk.k2, S);
+        sc_mul<5>(s2, hk.k2, S);
         int32_t fb[Bc2<W>::POS];
         sc_recode_w<W, Bc2<W>::POS>(fb, s2);
 #pragma unroll

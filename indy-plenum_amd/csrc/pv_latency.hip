@@ -198,7 +198,7 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
         lp_halfsize(c, hk, k);
         LAT_STAMP(12);
         uint32_t s2[8], fs[8], e1[8], e2[8];
-        sc_mul(s2, hk.k2, S);
+        sc_mul<5>(s2, hk.k2, S);
         LAT_STAMP(13);
         sc_recode65536(fs, s2);
         lu ent[PV_BCOMB_POS];
@@ -455,7 +455,7 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
         lp_halfsize(c, hk, k);
         LAT_STAMP(12);
         uint32_t s2[8], fs[8], e1[8], e2[8];
-        sc_mul(s2, hk.k2, S);
+        sc_mul<5>(s2, hk.k2, S);
         sc_recode65536(fs, s2);
         sc_recode16(e1, hk.k1);
         sc_recode16(e2, hk.k2);

@@ -209,7 +209,7 @@ static constexpr uint32_t SC_8L[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa
 #endif
 struct pv_halfk {
     uint32_t k1[8];  // |k1|
-    uint32_t k2[8];  // k2: odd, > 0
+    uint32_t k2[8];  // k2: odd, > 0, < 2^160 (words 5..7 zero: sc_mul<5>)
     bool neg;        // k1 = -|k1|
     bool fallback;   // (k, 1) was used
 };
@@ -574,12 +574,15 @@ PV_HD void sc_halfsize(pv_halfk& h, const uint32_t k[8], uint32_t* stats = nullp
 }
 
 // r = a * b mod L (a, b < 2^256)
+// NA: words of a that may be nonzero (a[NA..7] = 0: the split's k2 < 2^160 takes NA = 5, 40
+// word products instead of 64)
+template <int NA = 8>
 PV_HD void sc_mul(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
     uint32_t x[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) x[i] = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < NA; i++) {
         uint64_t c = 0;
 #pragma unroll
         for (int j = 0; j < 8; j++) {

@@ -560,7 +560,7 @@ PV_HD bool pv_prepare_half(ge_p3& PA, ge_p3& negR, pv_halfk& hk, uint32_t s2[8],
     uint32_t k[8];
     pv_hash_k(k, in, smlen, msgword);
     sc_halfsize(hk, k);
-    sc_mul(s2, hk.k2, in.S);
+    sc_mul<5>(s2, hk.k2, in.S);
     ge_p3_cneg(PA, hk.neg);
     return ok;
 }

@@ -429,7 +429,7 @@ int hc_sign_open_straus_half16(const uint8_t* sm, uint64_t smlen, const uint8_t*
             hk.k2[i] = i == 0 ? 1u : 0u;
         }
         hk.neg = false;
-        sc_mul(s2, hk.k2, in.S);
+        sc_mul<5>(s2, hk.k2, in.S);
     }
     HostATab at, rt;
     pv_build_a_table(at, PA);
@@ -581,7 +581,7 @@ int hc_lp_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
     pv_halfk hk;
     lp_halfsize(c, hk, k);
     uint32_t s2[8], fs[8], e1[8], e2[8];
-    sc_mul(s2, hk.k2, in.S);
+    sc_mul<5>(s2, hk.k2, in.S);
     sc_recode65536(fs, s2);
     lu ent[PV_BCOMB_POS];
     for (int j = 0; j < PV_BCOMB_POS; j++) ent[j] = lp_bcomb_entry(c, bcomb.data(), j, pv_half(fs[j >> 1], j));
@@ -631,7 +631,7 @@ int hc_lp4_sign_open(const uint8_t* sm, uint64_t smlen, const uint8_t* pk, int s
     pv_halfk hk;
     lp_halfsize(c, hk, k);
     uint32_t s2[8], fs[8], e1[8], e2[8];
-    sc_mul(s2, hk.k2, in.S);
+    sc_mul<5>(s2, hk.k2, in.S);
     sc_recode65536(fs, s2);
     sc_recode16(e1, hk.k1);
     sc_recode16(e2, hk.k2);
