@@ -423,7 +423,9 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
         return;
     }
     if (wave == 1) {
-        const bool sig_ok = pv_sig_ok(in, smlen);
+        // libsodium's checks on R, S, smlen, published before the hash: evaluated here, beside the
+        // SHA-512 call, instead of sunk behind it onto the critical path (2.6 us of dependent loads)
+        if (lane == 0) s_sig_ok = pv_sig_ok(in, smlen) ? 1u : 0u;
         if (cached) {
             uint32_t fs[8];
             sc_recode65536(fs, in.S);
@@ -436,7 +438,6 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
             if (lane == 0) {
 #pragma unroll
                 for (int q = 0; q < 8; q++) s_k256[q] = e256[q];
-                s_sig_ok = sig_ok ? 1u : 0u;
             }
             __syncthreads();  // 1
             s_part[0][lane] = lp_to_cached(c, lp_comb_b(c, [&](int j) -> lu { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); }), K.d2);
@@ -456,10 +457,12 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
         LAT_STAMP(12);
         uint32_t s2[8], fs[8], e1[8], e2[8];
         sc_mul<5>(s2, hk.k2, S);
+        LAT_STAMP(13);
         sc_recode65536(fs, s2);
         sc_recode16(e1, hk.k1);
         sc_recode16(e2, hk.k2);
         const int nw1 = sc_nwin16(e1), nw2 = sc_nwin16(e2);
+        LAT_STAMP(18);
         const int nw = __builtin_amdgcn_readfirstlane(nw1 > nw2 ? nw1 : nw2);
         if (lane == 0) {
 #pragma unroll
@@ -470,7 +473,6 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
             }
             s_nw = (uint32_t)nw;
             s_neg = hk.neg ? 1u : 0u;
-            s_sig_ok = sig_ok ? 1u : 0u;
         }
         LAT_STAMP(10);
         __syncthreads();  // 1

@@ -8,7 +8,8 @@ for the last call, block 0's s_memrealtime stamps (100 MHz) relative to wave 0's
   waves 2, 3 (four-wave form): 14 start, 7 / 15 y-only chain done (lp_ydbl_chain)
   wave 0, four-wave zero-copy form: 16 kernel entry, 17 request slot copied into LDS (negative:
           before wave 0's start)
-  wave 1: 8 start, 9 k ready, 12 split done, 13 k2 S mod L done, 10 digits and comb entries ready,
+  wave 1: 8 start, 9 k ready, 12 split done, 13 k2 S mod L done, 18 recodings done (four-wave),
+          10 digits and comb entries ready,
           11 [S]B / [k2](-R') + [s2]B done
 """
 import ctypes
@@ -38,7 +39,7 @@ def main():
         buf = (ctypes.c_ulonglong * 20)()
         assert L.pv_debug_lat_trace(buf) == 0
         t = list(buf)
-        runs.append({i: round((t[i] - t[0]) / 100.0, 2) for i in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17)})
+        runs.append({i: round((t[i] - t[0]) / 100.0, 2) for i in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18)})
         stats = {"lehmer_blocks": t[15] & 255, "block_quotients": (t[15] >> 8) & 255, "exact_steps": t[15] >> 16}
     med = {i: float(np.median([r[i] for r in runs])) for i in runs[0]}
     print(json.dumps({"lib": os.environ.get("PLENUM_AMD_LIB", "default"), "ok": bool(got[0]),
