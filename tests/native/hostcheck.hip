@@ -43,6 +43,7 @@ void hc_sc_reduce64(uint8_t* r, const uint8_t* x) {
 int hc_sc_is_canonical(const uint8_t* s) { uint32_t w[8]; load_words(w, s); return sc_is_canonical(w); }
 void hc_sc_recode16(uint8_t* out, const uint8_t* a) { uint32_t w[8], o[8]; load_words(w, a); sc_recode16(o, w); memcpy(out, o, 32); }
 void hc_sc_recode256(uint8_t* out, const uint8_t* a) { uint32_t w[8], o[8]; load_words(w, a); sc_recode256(o, w); memcpy(out, o, 32); }
+void hc_sc_recode65536(uint8_t* out, const uint8_t* a) { uint32_t w[8], o[8]; load_words(w, a); sc_recode65536(o, w); memcpy(out, o, 32); }
 int hc_has_small_order(const uint8_t* s) { uint32_t w[8]; load_words(w, s); return pv_has_small_order(w); }
 int hc_ge_is_canonical(const uint8_t* s) { uint32_t w[8]; load_words(w, s); return pv_ge_is_canonical(w); }
 

@@ -128,6 +128,20 @@ def test_scalar_reduce_canonical_recode(hc):
         assert all(-8 <= (n - 16 if n >= 8 else n) <= 8 for n in nib)
         hc.hc_sc_recode256(r, a.to_bytes(32, "little"))
         assert sum((b - 256 if b >= 128 else b) * 256 ** i for i, b in enumerate(r.raw)) == a
+        hc.hc_sc_recode65536(r, a.to_bytes(32, "little"))
+        hw = [int.from_bytes(r.raw[2 * i:2 * i + 2], "little") for i in range(16)]
+        assert sum((h - 65536 if h >= 32768 else h) * 65536 ** i for i, h in enumerate(hw)) == a
+    # the closed-form recodings ((a + M) xor M) against the digit-by-digit carry loop they replaced,
+    # for any 256-bit input (the top digit unreduced)
+    for a in [2 ** 256 - 1, 2 ** 255, 0x7777777777777777] + [rng.getrandbits(256) for _ in range(2000)]:
+        for w, fn in ((4, hc.hc_sc_recode16), (8, hc.hc_sc_recode256), (16, hc.hc_sc_recode65536)):
+            out, carry, n = 0, 0, 256 // w
+            for i in range(n):
+                v = ((a >> (w * i)) & ((1 << w) - 1)) + carry
+                carry = 0 if i == n - 1 else (v + (1 << (w - 1))) >> w
+                out |= ((v - (carry << w)) & ((1 << w) - 1)) << (w * i)
+            fn(r, a.to_bytes(32, "little"))
+            assert int.from_bytes(r.raw, "little") == out, (w, hex(a))
 
 
 def test_small_order_and_canonical_rules(hc):
