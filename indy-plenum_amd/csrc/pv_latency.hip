@@ -298,7 +298,7 @@ __global__ __launch_bounds__(LAT_THREADS) void pv_lat_kernel(const uint8_t* __re
 //   wave 0  sums the four parts, + R', compares with R' (lp_final_check).
 // A cached key keeps the two-wave cached flow (waves 2 and 3 only join the barriers).
 #ifndef PV_LAT4_MAX
-#define PV_LAT4_MAX 256  // batches up to this size take the four-wave form (more waves, less chain)
+#define PV_LAT4_MAX 512  // batches up to this size take the four-wave form (more waves, less chain)
 #endif
 #ifndef PV_LAT4_SPLIT
 #define PV_LAT4_SPLIT 17

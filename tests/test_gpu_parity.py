@@ -50,6 +50,18 @@ def test_each_adversarial_class_small_batches(native, sodium, oracle):
         assert np.array_equal(got, want), (cls, np.nonzero(got != want)[0][:5])
 
 
+def test_four_wave_cutoff_sizes(native, sodium, oracle):
+    """Batches on both sides of the latency path's four-wave / two-wave cutoff (PV_LAT4_MAX = 512,
+    and the round-3 cutoff 256), 2 % adversarial records included."""
+    g = VectorGen(sodium, oracle, seed=19)
+    cases = g.batch(513, adversarial_frac=0.02)
+    want = reference_verdicts(sodium, cases)
+    for n in (256, 257, 511, 512, 513):
+        blob, off, pks = pack(cases[:n])
+        got = native.verify_sm_batch(blob, off, pks)
+        assert np.array_equal(got, want[:n]), (n, np.nonzero(got != want[:n])[0][:10])
+
+
 def test_mixed_batch_2pct(native, sodium, oracle):
     g = VectorGen(sodium, oracle, seed=12)
     cases = g.batch(3000, adversarial_frac=0.02)

@@ -30,9 +30,10 @@ def build_hostcheck():
 
 @pytest.fixture(scope="module")
 def hc():
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
-            os.path.getmtime(os.path.join(ROOT, "indy-plenum_amd", "csrc", f))
-            for f in os.listdir(os.path.join(ROOT, "indy-plenum_amd", "csrc")) if f.endswith(".h")):
+    srcs = [os.path.join(ROOT, "indy-plenum_amd", "csrc", f)
+            for f in os.listdir(os.path.join(ROOT, "indy-plenum_amd", "csrc")) if f.endswith(".h")]
+    srcs.append(os.path.join(HERE, "native", "hostcheck.hip"))
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
         build_hostcheck()
     return ctypes.CDLL(LIB)
 
