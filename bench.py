@@ -250,6 +250,47 @@ def ingress_leg(n, blob, off, wire, steps, warmup):
     }
 
 
+H2D_PEAK_BPS = 57.5e9  # one pinned hipMemcpyAsync of 400 MB on the MI355X box (profiles/r05/h2d_bw.txt)
+
+
+def host_path_leg(blob, off, pks, want, reps=5):
+    """SURVEY.md §8e host traffic at N = 1: the whole configs[1] batch from host buffers through
+    pv_verify_batch (H2D of 131,072-request sub-batches on a copy stream beside the previous
+    sub-batch's kernels, verdicts back), median of `reps` calls after one that sizes the staging:
+      arena     the batch built in the library's pinned arena (pv_host_alloc: what a node that
+                receives into such buffers gets; the DMA reads the caller's bytes, no staging copy)
+      pageable  the same bytes in ordinary numpy memory (copy workers stage each sub-batch first)
+    Never `value`: the headline is device-resident."""
+    n = len(off) - 1
+    h2d_bytes = int(off[-1] - off[0]) + 32 * n + 8 * (n + 1)
+
+    def median_call(b, o, k):
+        _native.verify_sm_batch(b, o, k)
+        ts, ok = [], True
+        for _ in range(reps):
+            t1 = time.perf_counter()
+            v = _native.verify_sm_batch(b, o, k)
+            ts.append(time.perf_counter() - t1)
+            ok &= bool(np.array_equal(v, want))
+        med = float(np.median(ts))
+        return {"verifies_per_s": round(n / med, 1), "median_ms": round(1e3 * med, 3),
+                "min_ms": round(1e3 * min(ts), 3), "effective_h2d_GBps": round(h2d_bytes / med / 1e9, 2), "ok": ok}
+
+    page = median_call(blob, off, pks)
+    t0 = time.perf_counter()
+    ab, ao, ak = _native.HostArena.batch(blob, off, pks)
+    fill_s = time.perf_counter() - t0
+    arena = median_call(ab, ao, ak)
+    del ab, ao, ak
+    return dict(arena, requests=n, ok=arena["ok"] and page["ok"], form="arena", h2d_bytes=h2d_bytes,
+                pcie_bound_verifies_per_s=round(n / (h2d_bytes / H2D_PEAK_BPS), 1),
+                frac_of_pcie_bound=round(arena["verifies_per_s"] / (n / (h2d_bytes / H2D_PEAK_BPS)), 4),
+                arena_fill_s=round(fill_s, 3), pageable=page,
+                note="pv_verify_batch on the headline batch (tampered records included, verdicts checked) from "
+                     "host memory, PCIe included; pipelined sub-batches of 131,072 requests; "
+                     "pcie_bound = the H2D bytes at the box's measured %.1f GB/s" % (H2D_PEAK_BPS / 1e9))
+
+
 def multisig_reduce(bits_nk):
     """authenticate_multi with threshold None (client_authn.py:84-118) over verdict bits (n, k) in
     dict order: a request is accepted iff all k signatures verify; a rejected one raises
@@ -291,20 +332,23 @@ def multisig_leg(multi, n_req, k, steps):
                     "device-resident, one launch per step; ~1 % of records have a flipped R/S bit"}
 
 
-def config1_python(wire, k=10000):
+def config1_python(wire, k=10000, gpu=False):
     """configs[0] of BASELINE.json: k signed NYM requests through CoreAuthNr.authenticate one at a
     time on one host core, each signature checked by libsodium 1.0.18 crypto_sign_open (what the
     reference's node does per request: json.loads -> Request -> ReqAuthenticator.authenticate ->
     DidVerifier -> libnacl). The drop-in Python classes stand in for the reference's (golden-pinned
-    in tests/test_host_logic.py); libsodium is called through ctypes as libnacl does. CPU leg only."""
+    in tests/test_host_logic.py); libsodium is called through ctypes as libnacl does. CPU leg only.
+    gpu=True: the same loop with the HIP engine and no batch context -- the unmodified drop-in per-call
+    pattern (nacl_wrappers.py:232-242 inside client_authn.py:84-118, reached from node.py:2624): every
+    signature is one pv_verify_batch call of ONE request (the zero-copy latency kernel)."""
     from oracle.libsodium_ref import LibSodium, find_libsodium
     from plenum_amd import batch
     from plenum_amd.client_authn import CoreAuthNr
     from plenum_amd.req_authenticator import ReqAuthenticator
     from plenum_amd.wire import Request
-    if find_libsodium() is None:
+    if find_libsodium() is None and not gpu:
         return None
-    sodium = LibSodium()
+    sodium = None if gpu else LibSodium()
     wblob, woff = wire[0], wire[1]
     k = min(k, len(woff) - 1)
     pool = nym_workload._pool()
@@ -319,6 +363,23 @@ def config1_python(wire, k=10000):
         return [sodium.sign_open_ok(blob.tobytes(), pks[0].tobytes())]
 
     ok = 0
+    if gpu:  # no batch context: plenum_amd.batch.verdict() makes one engine call per signature
+        for raw in raws[:200]:  # warm-up: staging sized, clocks up
+            req = Request(**json.loads(raw.decode()))
+            ra.authenticate(req.as_dict, req.key)
+        ra = ReqAuthenticator()
+        ra.register_authenticator(core)
+        t0 = time.perf_counter()
+        for i, raw in enumerate(raws):
+            req = Request(**json.loads(raw.decode()))
+            ok += ra.authenticate(req.as_dict, req.key) == {pool[i % len(pool)]["did"]}
+        dt = time.perf_counter() - t0
+        return {"requests": k, "cores": 1, "requests_per_s": round(k / dt, 1),
+                "us_per_request": round(dt * 1e6 / k, 1), "accepted": ok,
+                "note": "configs[0] through the drop-in surface with the HIP engine and NO batching: per-request "
+                        "json.loads + Request + ReqAuthenticator.authenticate, each signature one pv_verify_batch "
+                        "call of one request (what an unmodified Node.verifySignature gets; the feed points "
+                        "authenticate_client_quota / authenticate_propagates batch instead)"}
     t0 = time.perf_counter()
     with batch.active(batch.VerdictCache(), engine):
         for i, raw in enumerate(raws):
@@ -400,6 +461,7 @@ def pmc_valu_issue(kernel, cus=256):
         return None
 
 
+FUSED_MIN_REQ = 262144  # pv_comb_ab_kernel runs for chunks above this (PV_FUSED_MIN_REQ), else pv_comb_a_kernel
 CONFIG5_TOTAL = 1 << 26  # configs[4]: 64M requests over the node's GPUs
 
 
@@ -572,6 +634,27 @@ def add_cpu_baseline(result, cb, c1=None):
     if c1:
         result["cpu_baseline"]["config1_python_authenticate"] = c1
     return result
+
+
+def feed_point_crossover(result):
+    """The smallest host-buffer batch (of the measured sizes) whose verifies/s beat libsodium on all the
+    host cores the cpu_baseline used, and the per-call drop-in against libsodium's own per-call loop:
+    the numbers INTEGRATION.md §1 states (feed-point batching is required, not optional)."""
+    cb = result.get("cpu_baseline", {}).get("value")
+    lat = result.get("host_path", {}).get("batch_latency")
+    if not cb or not lat:
+        return
+    sizes = sorted(int(k) for k in lat if k.isdigit())
+    beat = [k for k in sizes if lat[str(k)]["verifies_per_s"] > cb]
+    out = {"cpu_baseline_verifies_per_s": cb, "cores": result["cpu_baseline"].get("cores"),
+           "smallest_batch_beating_cpu": beat[0] if beat else None,
+           "per_size_verifies_per_s": {str(k): lat[str(k)]["verifies_per_s"] for k in sizes}}
+    one = result.get("drop_in_per_call")
+    c1 = result.get("cpu_baseline", {}).get("config1_python_authenticate")
+    if one and c1:
+        out["per_call_requests_per_s"] = {"gpu_unbatched": one["requests_per_s"], "libsodium_one_core": c1["requests_per_s"],
+                                          "ratio": round(one["requests_per_s"] / c1["requests_per_s"], 3)}
+    result["feed_point_crossover"] = out
 
 
 class FileBarrier:
@@ -862,7 +945,7 @@ def main():
 
     result = assemble_result(world, n, args.steps, args.warmup, elapsed, stage_ms, chunks, comb, nkeys,
                              float(blob.nbytes) / n, ok_local, ok_all, per_gpu_fixed=bool(args.per_gpu),
-                             fused=_native.comb_fused())
+                             fused=_native.comb_fused() and n / chunks > FUSED_MIN_REQ)
     if world > 1 and not args.no_host_path:
         # SURVEY.md §8e host traffic: each rank's shard from host buffers (pv_verify_batch: pinned
         # staging pipelined with the H2D DMA, kernels, verdicts back), on up to configs[4]'s 8M-request
@@ -916,14 +999,10 @@ def main():
         c3, c3_got, c3_batch = config3_leg(db, blob0, off, pks, max(3, args.steps), args.warmup, timed)
         result["config3"] = c3
     if rank == 0 and world == 1 and not args.no_host_path:
-        # PCIe-inclusive host-buffer path (pv_verify_batch): staging copy + H2D + kernels + D2H
-        hsamp = min(n, 1 << 18)
-        hoff = off[:hsamp + 1]
-        _native.verify_sm_batch(blob0[:int(hoff[-1])], hoff, pks[:hsamp])
-        t1 = time.perf_counter()
-        v = _native.verify_sm_batch(blob0[:int(hoff[-1])], hoff, pks[:hsamp])
-        dt = time.perf_counter() - t1
-        result["host_path"] = {"verifies_per_s": round(hsamp / dt, 1), "requests": hsamp, "ok": bool(v.all())}
+        # PCIe-inclusive host-buffer path (pv_verify_batch) on the headline batch itself
+        t0 = time.perf_counter()
+        result["host_path"] = host_path_leg(blob, off, pks, want_local)
+        phases["host_path"] = time.perf_counter() - t0
         # latency of one host-buffer call at the batch sizes Plenum's feed points produce (a ZStack
         # client quota is 100 messages, a node quota 1,000): median of 200 calls (50
         # above 4,096 requests) after 20 untimed ones, AUTO
@@ -948,7 +1027,7 @@ def main():
                 lat[str(k)] = {"median_ms": round(1e3 * med, 3), "verifies_per_s": round(k / med, 1),
                                "path": _native.last_path()[0], "ok": okk}
             return lat
-        lat = latency_at((1, 100, 1000, 4096, 10000, 32768))
+        lat = latency_at((1, 2, 4, 8, 16, 32, 64, 100, 1000, 4096, 10000, 32768))
 
         # the device-buffer call at 2,049-4,096 requests: AUTO's latency-vs-keyed choice is made on
         # the device by the dedup kernels (no host key count); median of 20 enqueue+sync rounds
@@ -1011,6 +1090,12 @@ def main():
         result["host_path"]["batch_latency"] = lat
         result["host_prep"] = {"workload_generation_s": round(gen_s, 2), "note": "serialize + sign, %d workers" % min(
             16, os.cpu_count() or 1)}
+    if rank == 0 and world == 1 and wire and not args.no_host_path:
+        # configs[0] through the unmodified per-call drop-in with the HIP engine (one launch per
+        # signature), beside the libsodium leg of the same loop (cpu_baseline.config1_python_authenticate)
+        t0 = time.perf_counter()
+        result["drop_in_per_call"] = config1_python(wire, gpu=True)
+        phases["drop_in_per_call"] = time.perf_counter() - t0
     if multi is not None:
         result["multisig"] = multisig_leg(multi, min(n, 1 << 20), 3, max(3, args.steps // 4))
     if rank == 0 and world == 1 and wire:
@@ -1032,6 +1117,7 @@ def main():
             cb, c3_want = cpu_baseline(blob0, off, pks, min(args.cpu_sample, n), args.cpu_seconds,
                                        config3=c3_batch if c3 else None)
             add_cpu_baseline(result, cb, c1)
+            feed_point_crossover(result)
             if c3 is not None:
                 c3["verdicts_match_libsodium"] = bool(np.array_equal(c3_got, c3_want))
                 c3["mismatches"] = int((c3_got != c3_want).sum())

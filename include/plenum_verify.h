@@ -78,7 +78,13 @@ void pv_shutdown(void);
 const char* pv_last_error(void);
 
 /* Host buffers in, host bitmap out (ceil(n/8) bytes). sm_off has n+1 entries, non-decreasing;
- * offsets need no alignment (the library copies into its own pinned staging buffer). Synchronous.
+ * offsets need no alignment. Synchronous. Inputs in ordinary (pageable) memory are copied into the
+ * library's pinned staging buffer by per-device copy threads; inputs that lie in pinned memory the
+ * library allocated or registered (pv_host_alloc / pv_host_register below) are DMA'd from where they
+ * are, without that copy (the offsets too when sm_off[0] == 0). Batches whose blob is >= 8 MB are
+ * verified in sub-batches of 131,072 requests whose H2D transfers (on a copy stream) overlap the
+ * previous sub-batch's kernels, so a large host batch costs about its PCIe time plus one sub-batch's
+ * kernels.
  * A call of <= 2,048 requests that takes the latency path (AUTO's range for host buffers without a
  * key-repeat hint, or PV_PATH_LATENCY) and whose records are all <= 1,840 bytes is zero-copy: the
  * requests go into fixed-stride slots of the pinned staging buffer that the kernel reads over PCIe,
@@ -112,6 +118,31 @@ int pv_verify_batch_multi_gpu(const uint8_t* sm, const uint64_t* sm_off, uint64_
                               uint8_t* verdict_bits);
 int pv_multi_gpu_devices(int* devices, int max_devices);
 int pv_shard_plan(uint64_t n, int ndev, uint64_t* bounds, uint64_t* words_per_shard);
+
+/* Library-owned pinned host memory: the host-fed path's input arena. A node that receives its
+ * requests straight into such buffers (the signature + message blob, the offsets, the keys) lets
+ * pv_verify_batch / pv_verify_batch_multi_gpu DMA them to HBM without a pageable -> pinned copy. The
+ * blocks are portable (every device of the process can DMA from them). Any range inside a block is
+ * recognised per call.
+ *   pv_host_alloc(p, bytes)      allocate a pinned block (*p = its address)
+ *   pv_host_free(p)              free a pv_host_alloc block (PV_ERR_ARG for any other pointer)
+ *   pv_host_register(p, bytes)   pin an existing host range in place (hipHostRegister; ~50 ms per GB,
+ *                                for long-lived receive buffers)
+ *   pv_host_unregister(p)        undo pv_host_register (p = the registered start)
+ *   pv_host_is_pinned(p, bytes)  1 if [p, p + bytes) lies inside one such block or range */
+int pv_host_alloc(void** p, uint64_t bytes);
+int pv_host_free(void* p);
+int pv_host_register(void* p, uint64_t bytes);
+int pv_host_unregister(void* p);
+int pv_host_is_pinned(const void* p, uint64_t bytes);
+
+/* Test hook (fault injection, for the failure-path tests): PV_INJECT_STAGE makes the next `count`
+ * host-buffer stagings on `device` (pv_verify_batch's copy form, a shard of pv_verify_batch_multi_gpu)
+ * fail as an allocation failure would -- in the pipelined form after the first sub-batch's DMA and
+ * kernels were enqueued -- so the tests can check that the call returns an error only after no copy
+ * still reads the buffers, and that the next call is exact. count 0 clears it. */
+#define PV_INJECT_STAGE 1
+int pv_test_inject(int what, int device, int count);
 
 /* Device buffers in, device bitmap out. Requirements: d_sm 4-byte aligned and readable up to
  * sm_off[n] + PV_BLOB_SLACK (records themselves need no alignment), d_pk 16-byte aligned,

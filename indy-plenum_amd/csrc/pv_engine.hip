@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "btable.h"
+#include "copy_pool.h"
 #include "comb.h"
 #include "keycache.h"
 #include "lp25519.h"
@@ -92,6 +93,8 @@ static constexpr uint32_t PV_KEY_CAP = 16384;     // distinct keys the comb tabl
 static constexpr uint64_t PV_KEYED_MIN = 4097;
 static constexpr uint32_t PV_ALLCOMB_KEYS = 2048;
 static constexpr uint32_t PV_ALLCOMB_CHUNK = 262144;
+static constexpr uint32_t PV_XT_KEYS = 2048;      // tables shared by a pipelined call's sub-batches (1.35 GB)
+static constexpr uint32_t PV_XT_HASH = 4096;      // their hash table (>= 2 x keys)
 // An all-comb chunk of at most PV_SPARSE_CHUNK requests and at most PV_SPARSE_PER_KEY requests per key
 // on average builds only the table entries its digits use (comb.h pv_comb_fill_sparse; the need
 // masks are set by pv_comb_prep_kernel). A/B on MI355X (1,024 signers, device time,
@@ -441,6 +444,7 @@ struct KeyWork {
     uint32_t chunk_n;  // requests in this chunk
     uint32_t lat_choice;  // the scan picks latency vs keyed for this chunk (AUTO, device-buffer call)
     uint32_t seg_cap;     // key ids of segment s are s * seg_cap + [0, its counter)
+    uint32_t dense_only;  // never fill sparsely (the tables outlive the chunk: pv_xtab_publish_kernel)
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
 #ifndef PV_COMB_MIN_REQ
@@ -1016,6 +1020,30 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_cache_probe_kernel(const uint
     kw.key_cslot[id] = pv_kc_lookup(kc, A);
 }
 
+// Tables shared by the sub-batches of one pipelined host call (stage_and_launch): sub-batch 0 builds
+// its comb keys' tables straight into the call's table store (kw.ctab points there), then this kernel
+// publishes them as a key-cache view -- comb index j = slot j: its key's bytes and libsodium flag, and j
+// inserted into the view's open-addressing hash table (cleared before the call) -- so the later
+// sub-batches find those keys with the cache probe and read the tables instead of rebuilding them.
+__global__ __launch_bounds__(PV_BLOCK) void pv_xtab_publish_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
+                                                                    uint32_t* __restrict__ htab, uint32_t hmask,
+                                                                    uint32_t seed, uint32_t* __restrict__ keys,
+                                                                    uint32_t* __restrict__ flags) {
+    const uint32_t j = blockIdx.x * PV_BLOCK + threadIdx.x;
+    if (j >= kw.nkeys[PV_SPLIT_COMB_KEYS] || kw.comb_cslot[j] != PV_EMPTY) return;
+    uint32_t A[8];
+    pv_load_pk(A, pk, kw.key_owner[kw.comb_key[j]]);
+#pragma unroll
+    for (int q = 0; q < 8; q++) keys[8 * j + q] = A[q];
+    flags[j] = kw.key_flag[j];
+    __threadfence();  // the key bytes before the hash entry that names them
+    uint32_t h = pv_kc_hash(A, seed) & hmask;
+    for (uint32_t probe = 0; probe <= hmask; probe++) {  // distinct keys, hmask + 1 >= 2 x entries
+        if (atomicCAS(&htab[h], PV_KC_EMPTY, j) == PV_KC_EMPTY) return;
+        h = (h + 1) & hmask;
+    }
+}
+
 // Exclusive prefix sum of one value per thread over a 1024-thread workgroup; *total = the sum.
 #ifndef PV_SCAN_WAVE
 #define PV_SCAN_WAVE 1
@@ -1155,7 +1183,7 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
         kw.nkeys[PV_SPLIT_COMB_KEYS] = min(ncand, kw.kcap);
         kw.nkeys[PV_SPLIT_SLOTS] = ctotal;
         kw.nkeys[PV_SPLIT_SPARSE] =
-            all_comb && kw.chunk_n <= PV_SPARSE_CHUNK && kw.chunk_n <= PV_SPARSE_PER_KEY * nk ? 1u : 0u;
+            !kw.dense_only && all_comb && kw.chunk_n <= PV_SPARSE_CHUNK && kw.chunk_n <= PV_SPARSE_PER_KEY * nk ? 1u : 0u;
     }
 }
 
@@ -2131,6 +2159,24 @@ struct Ctx {
     uint64_t h_stage_cap = 0;
     uint8_t* d_stage = nullptr;
     uint64_t d_stage_cap = 0;
+    uint64_t* h_ver = nullptr;  // pinned verdict words of the pipelined host-buffer form
+    uint64_t h_ver_cap = 0;
+    // pipelined host-buffer form: H2D of sub-batch j on cstream, its kernels on `stream` after ev_copy[j]
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_cstart = nullptr;  // the engine stream's work so far (cstream waits: staging reuse)
+    std::vector<hipEvent_t> ev_copy;
+    int inject_stage = 0;  // pv_test_inject(PV_INJECT_STAGE): host-buffer stagings left to fail
+    // the comb tables one pipelined host call's sub-batches share (pv_xtab_publish_kernel): room for
+    // PV_XT_KEYS keys, allocated on first use; xt_fill: the next chunk builds its tables here and
+    // publishes them; xt_use: the next chunks look keys up here (as in the node-side key cache)
+    struct {
+        uint32_t* htab = nullptr;
+        uint32_t* keys = nullptr;
+        uint32_t* flags = nullptr;
+        uint4* tab = nullptr;
+        bool failed = false;  // allocation failed once: the call's sub-batches build their own tables
+    } xt;
+    bool xt_fill = false, xt_use = false;
     bool timing = false;
     // PV_NSTAGES + 1 events per chunk launched since pv_set_timing(1) (stage boundaries, see
     // pv_stage_times); unused stages record back-to-back events
@@ -2394,7 +2440,14 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
         // Chunks below PV_KEYED_MIN (the latency path's range; only the tail chunk of a large
         // batch can be that small) skip dedup and go Straus. A key in the node-side key cache has
         // its comb table already built: its requests take the comb path at any count.
-        const PvKeyCacheView kcv = kc_view();
+        PvKeyCacheView kcv = kc_view();
+        const uint32_t* kc_flags = g_ctx.kc.d_flags;
+        const uint4* kc_tab = g_ctx.kc.d_tab;
+        if (g_ctx.xt_use) {  // a later sub-batch of a pipelined host call: the call's shared tables
+            kcv = PvKeyCacheView{g_ctx.xt.htab, g_ctx.xt.keys, g_ctx.xt.flags, g_ctx.xt.tab, PV_XT_HASH - 1, g_ctx.kw.seed};
+            kc_flags = g_ctx.xt.flags;
+            kc_tab = g_ctx.xt.tab;
+        }
         const bool kc_active = kcv.hmask != 0;
         const bool keyed = g_ctx.path == PV_PATH_COMB ||
                            (g_ctx.path == PV_PATH_AUTO &&
@@ -2409,7 +2462,13 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
         // a key-id segment holds the owners among its waves (every PV_NSEG-th wave of the chunk)
         kw.seg_cap = (uint32_t)((((m + 63) / 64) + PV_NSEG - 1) / PV_NSEG * 64);
         kw.lat_choice = dev_choice ? 1u : 0u;
-        kw.kc_tab = g_ctx.kc.d_tab;
+        kw.kc_tab = kc_tab;
+        kw.dense_only = 0;
+        if (g_ctx.xt_fill) {  // sub-batch 0 of a pipelined host call: its tables go to the shared store, whole
+            kw.ctab = g_ctx.xt.tab;
+            kw.kcap = std::min<uint32_t>(kw.kcap, PV_XT_KEYS);
+            kw.dense_only = 1;
+        }
         const uint32_t limit = kw.kcap;  // comb keys a chunk can hold (launch grids of the key stream)
         const bool direct_fill = PV_CHAIN_MODE == 2 && PV_CHAIN_PARTS == 1 && PV_DIRECT_FILL && m > PV_SPARSE_CHUNK;
         if (keyed) {
@@ -2467,8 +2526,7 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             }
             gate = Gate{kw.nkeys, kw.slot_req};
             // key-sorted slot order: comb keys' requests first, then the Straus requests
-            hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(PV_SCAN_THREADS), 0, stream, kw,
-                               (const uint32_t*)g_ctx.kc.d_flags);
+            hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(PV_SCAN_THREADS), 0, stream, kw, kc_flags);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             hipLaunchKernelGGL(pv_key_scatter_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -2625,6 +2683,12 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
                                d_verdict + c0 / 64, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             g_ctx.slots_dirty = false;
+            if (g_ctx.xt_fill) {  // publish this chunk's tables for the call's later sub-batches
+                hipLaunchKernelGGL(pv_xtab_publish_kernel, dim3(PV_XT_KEYS / PV_BLOCK), dim3(PV_BLOCK), 0, stream,
+                                   d_pk + 32 * c0, kw, g_ctx.xt.htab, PV_XT_HASH - 1, g_ctx.kw.seed, g_ctx.xt.keys,
+                                   g_ctx.xt.flags);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            }
             if (dev_choice) {  // runs only when the scan picked latency (the words were zeroed above)
                 rc = pv_latency_launch(d_sm, d_off + c0, m, d_pk + 32 * c0, g_ctx.d_bcomb, kc_view(),
                                        d_verdict + c0 / 64, true, stream, kw.nkeys + PV_SPLIT_LAT);
@@ -2719,9 +2783,10 @@ void lane_free_buffers(Work& w, KeyWork& kw) {
     kw = KeyWork{};
 }
 
+void ctx_free();
 // Builds g_ctxs[device] (caller: g_mus[device] held, DevScope(device) active, context not built yet):
 // streams and events, the fixed-base tables, the workspace. Sets the calling thread's HIP device.
-int ctx_init(int device) {
+int ctx_init_parts(int device) {
     PV_HIP(hipSetDevice(device), PV_ERR_NO_DEVICE);
     hipDeviceProp_t prop;
     PV_HIP(hipGetDeviceProperties(&prop, device), PV_ERR_NO_DEVICE);
@@ -2756,11 +2821,24 @@ int ctx_init(int device) {
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
 #endif
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+#if PV_COMB_B_EARLY
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.bstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
+#endif
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_start, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_verdict_copied, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    {
+        // the host path's copy stream at the greatest priority: the runtime keeps such streams on hardware
+        // queues of their own instead of round-robin over GPU_MAX_HW_QUEUES (4) with the engine's streams,
+        // where a copy sat behind the key stream's table fill (profiles/r05/host_path)
+        int least = 0, greatest = 0;
+        PV_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest), PV_ERR_NO_DEVICE);
+        const char* pe = getenv("PV_CSTREAM_PRIO");  // A/B knob: 0 = normal priority
+        const bool hi = !(pe && *pe == '0');
+        PV_HIP(hipStreamCreateWithPriority(&g_ctx.cstream, hipStreamNonBlocking, hi ? greatest : least), PV_ERR_NO_DEVICE);
+    }
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_cstart, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     std::vector<uint32_t> bt(PV_BTAB_ENTRIES * PV_BTAB_STRIDE);
     pv_build_b_table(bt.data());
     PV_HIP(hipMalloc((void**)&g_ctx.d_btab, bt.size() * 4), PV_ERR_ALLOC);
@@ -2839,6 +2917,20 @@ int ctx_init(int device) {
     return PV_OK;
 }
 
+// ctx_init_parts, and on failure everything it had built is released (streams, events, the workspace,
+// the tables): a retry of pv_init / pv_init_devices starts from an empty context instead of allocating
+// ~25 GB on top of a half-built one.
+int ctx_init(int device) {
+    const int rc = ctx_init_parts(device);
+    if (rc != PV_OK) {
+        const std::string err = g_err;
+        g_ctx.device = device;  // ctx_free releases a context of a known device
+        ctx_free();
+        g_err = err;
+    }
+    return rc;
+}
+
 // Frees g_ctxs[t_dev or primary] (caller holds its mutex).
 void ctx_free() {
     if (g_ctx.device < 0) return;
@@ -2870,6 +2962,12 @@ void ctx_free() {
     if (g_ctx.ev_straus_done) (void)hipEventDestroy(g_ctx.ev_straus_done);
     if (g_ctx.ev_launch_done) (void)hipEventDestroy(g_ctx.ev_launch_done);
     if (g_ctx.ev_verdict_copied) (void)hipEventDestroy(g_ctx.ev_verdict_copied);
+    if (g_ctx.cstream) (void)hipStreamDestroy(g_ctx.cstream);
+    if (g_ctx.ev_cstart) (void)hipEventDestroy(g_ctx.ev_cstart);
+    for (hipEvent_t e : g_ctx.ev_copy) (void)hipEventDestroy(e);
+    if (g_ctx.h_ver) (void)hipHostFree(g_ctx.h_ver);
+    for (void* p : {(void*)g_ctx.xt.htab, (void*)g_ctx.xt.keys, (void*)g_ctx.xt.flags, (void*)g_ctx.xt.tab})
+        if (p) (void)hipFree(p);
     if (g_ctx.kc.ev_async) (void)hipEventDestroy(g_ctx.kc.ev_async);
     g_ctx = Ctx();
 }
@@ -3009,84 +3107,21 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
     return launch(d_sm, d_off, n, d_pk, d_verdict_words, stream ? (hipStream_t)stream : g_ctx.stream);
 }
 
-// Host-side copy pool for the host-buffer entry: persistent threads (created on first use, at most 8,
-// half the host's hardware threads), so a call pays no thread creation. run(k, fn) executes fn(0..k-1)
-// on the pool and the calling thread and returns when all are done. Calls from several threads (the
-// per-device workers of pv_verify_batch_multi_gpu, contexts of different devices) take turns.
-class CopyPool {
-   public:
-    void run(unsigned k, const std::function<void(unsigned)>& fn) {
-        if (k <= 1) {
-            for (unsigned i = 0; i < k; i++) fn(i);
-            return;
-        }
-        std::lock_guard<std::mutex> turn(run_mu_);
-        if (workers() == 0) {
-            for (unsigned i = 0; i < k; i++) fn(i);
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            fn_ = &fn;
-            next_ = 0;
-            total_ = k;
-            done_ = 0;
-            gen_++;
-        }
-        cv_.notify_all();
-        drain();
-        std::unique_lock<std::mutex> lk(m_);
-        done_cv_.wait(lk, [&] { return done_ == total_; });
-        fn_ = nullptr;
-    }
-
-   private:
-    unsigned workers() {
-        if (!started_) {
-            started_ = true;
-            const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-            const unsigned nw = std::min(8u, hw / 2);
-            for (unsigned i = 0; i + 1 < nw; i++) th_.emplace_back([this] { loop(); });
-        }
-        return (unsigned)th_.size();
-    }
-    void drain() {  // take tasks until none is left
-        for (;;) {
-            unsigned i;
-            const std::function<void(unsigned)>* f;
-            {
-                std::lock_guard<std::mutex> lk(m_);
-                if (!fn_ || next_ >= total_) return;
-                i = next_++;
-                f = fn_;
-            }
-            (*f)(i);
-            std::lock_guard<std::mutex> lk(m_);
-            if (++done_ == total_) done_cv_.notify_all();
-        }
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
-            }
-            drain();
-        }
-    }
-    std::mutex m_, run_mu_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(unsigned)>* fn_ = nullptr;
-    unsigned next_ = 0, total_ = 0, done_ = 0;
-    uint64_t gen_ = 0;
-    bool started_ = false;
-    std::vector<std::thread> th_;
-};
-// never destroyed: its threads sleep on the condition variable until the process ends (a forked child,
-// which has none of them, must not run a destructor that joins them)
-CopyPool& g_copy_pool = *new CopyPool;
+// Host-side copy workers (copy_pool.h): one pool per device context, so the per-device workers of
+// pv_verify_batch_multi_gpu stage their shards at the same time; pinned host ranges the library owns
+// or registered (pv_host_alloc / pv_host_register), whose bytes the host-buffer entry DMAs directly.
+}  // extern "C"
+namespace {
+pvhost::PinnedRegistry g_pinned_alloc, g_pinned_reg;
+bool pv_is_pinned(const void* p, uint64_t bytes) {
+    return g_pinned_alloc.contains(p, bytes) || g_pinned_reg.contains(p, bytes);
+}
+pvhost::CopyPool& cur_pool() {
+    static const unsigned ndev = (unsigned)std::max(1, pv_device_count());
+    return pvhost::copy_pool_for<PV_MAX_DEV>(pv_cur_dev(), ndev);
+}
+}  // namespace
+extern "C" {
 
 // Move the request blob host -> pinned staging -> HBM. One host thread copies ~10 GB/s, so the blob is
 // cut into pieces (256 KB - 4 MB) that the copy pool stages in parallel; with `dma`, each piece's DMA
@@ -3098,7 +3133,7 @@ static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* s
     const uint64_t piece = std::min<uint64_t>(4ull << 20, std::max<uint64_t>(256ull << 10, bytes / 16));
     const unsigned k = (unsigned)((bytes + piece - 1) / piece);
     std::atomic<int> err{0};
-    g_copy_pool.run(k, [&](unsigned i) {
+    cur_pool().run(k, [&](unsigned i) {
         const uint64_t o = (uint64_t)i * piece, e = std::min(bytes, o + piece);
         memcpy(h_stage + o, src + o, e - o);
         if (dma && hipMemcpyAsync(d_dst + o, h_stage + o, e - o, hipMemcpyHostToDevice, s) != hipSuccess) err = 1;
@@ -3190,7 +3225,7 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
                 fill_at(slots, 0, n);
             } else {  // node-quota sizes: the slots are written by the copy pool's threads
                 const unsigned k = 8;
-                g_copy_pool.run(k, [&](unsigned t) { fill_at(slots, n * t / k, n * (t + 1) / k); });
+                cur_pool().run(k, [&](unsigned t) { fill_at(slots, n * t / k, n * (t + 1) / k); });
             }
             hipStream_t s = g_ctx.stream;
             if (g_ctx.last_stream && g_ctx.last_stream != s)
@@ -3225,72 +3260,245 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     return PV_OK;
 }
 
-// The copy form of a host-buffer batch on the calling thread's context: stages the keys, offsets and
-// records into the pinned / device staging areas (pipelined with the H2D DMA for large blobs) and
-// enqueues the verification on the context's stream. d_out: where the verdict words go (nullptr =
-// the staging area's own verdict section); *dver / *hver receive the staging area's device / pinned
-// verdict sections.
+// Requests per sub-batch of the pipelined host-buffer form (a multiple of 64; env PV_PIPE_SUB overrides
+// it for A/Bs). Sub-batch j's H2D runs on the copy stream while sub-batch j-1's kernels run, so a large
+// host batch costs about its PCIe time plus the last sub-batch's kernels instead of their sum.
+#ifndef PV_PIPE_SUB
+#define PV_PIPE_SUB 131072
+#endif
+static constexpr uint64_t PV_PIPE_MAX = 64;                // sub-batches per call (copy events)
+static constexpr uint64_t PV_PIPE_MIN_BLOB = 8ull << 20;   // smaller blobs: one piece
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+static uint64_t pipe_sub() {
+    static const uint64_t v = [] {
+        const char* e = getenv("PV_PIPE_SUB");
+        const uint64_t x = e && *e ? strtoull(e, nullptr, 10) : (uint64_t)PV_PIPE_SUB;
+        return std::max<uint64_t>(8192, x / 64 * 64);
+    }();
+    return v;
+}
+
+// The shared-table store of the pipelined host path (on first use; a failed allocation is not retried:
+// the sub-batches then build their own tables, same verdicts).
+static int ensure_xtab() {
+    auto& x = g_ctx.xt;
+    if (x.tab) return PV_OK;
+    if (x.failed) return PV_ERR_ALLOC;
+    if (hipMalloc((void**)&x.htab, PV_XT_HASH * 4) != hipSuccess ||
+        hipMalloc((void**)&x.keys, PV_XT_KEYS * 32) != hipSuccess ||
+        hipMalloc((void**)&x.flags, PV_XT_KEYS * 4) != hipSuccess ||
+        hipMalloc((void**)&x.tab, (uint64_t)PV_XT_KEYS * PV_COMB_POS * PV_COMB_ENT * 160) != hipSuccess) {
+        (void)hipGetLastError();
+        for (void* p : {(void*)x.htab, (void*)x.keys, (void*)x.flags, (void*)x.tab})
+            if (p) (void)hipFree(p);
+        x.htab = x.keys = x.flags = nullptr;
+        x.tab = nullptr;
+        x.failed = true;
+        return PV_ERR_ALLOC;
+    }
+    return PV_OK;
+}
+
+static int ensure_hver(uint64_t bytes) {
+    if (bytes <= g_ctx.h_ver_cap) return PV_OK;
+    if (g_ctx.h_ver) (void)hipHostFree(g_ctx.h_ver);
+    g_ctx.h_ver = nullptr;
+    g_ctx.h_ver_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(bytes, 64 << 10);
+    PV_HIP(hipHostMalloc((void**)&g_ctx.h_ver, cap, hipHostMallocPortable), PV_ERR_ALLOC);
+    g_ctx.h_ver_cap = cap;
+    return PV_OK;
+}
+
+// The copy form of a host-buffer batch on the calling thread's context: moves the keys, offsets and
+// records to the device staging area and enqueues the verification on the context's stream. d_out:
+// where the verdict words go (nullptr = the staging area's own verdict section); *dver / *hver receive
+// the device verdict section and a pinned buffer for the caller's copy back.
+//   * small batches (blob < 8 MB, no input in pinned memory): one host copy into pinned staging in the
+//     device layout, one DMA, the kernels (the quota sizes: fewest packets on the path);
+//   * otherwise, in sub-batches of pipe_sub() requests: the copy workers stage sub-batch j's pageable
+//     inputs (inputs inside pv_host_alloc / pv_host_register memory are not copied: the DMA reads them
+//     where they are), its H2D goes on the copy stream, and its kernels on the engine stream after an
+//     event -- so PCIe, host staging and kernels of consecutive sub-batches overlap.
+// Staging layout (host and device, 256-B aligned sections): [pk n*32][off (n+1) u64][verdict][blob +
+// PV_BLOB_SLACK]. A failure after DMAs were enqueued returns only after both streams drained, so no copy
+// still reads the caller's or the staging buffers.
 static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk, uint64_t* d_out,
                             uint64_t** dver_out, uint64_t** hver_out) {
-    g_ctx.last_zero_copy = false;
-    // staging layout (one pinned buffer, one device buffer, 256-B aligned sections):
-    //   [pk n*32][off (n+1) u64][verdict ceil(n/64) u64][blob + PV_BLOB_SLACK]
+    Ctx& c = g_ctx;
+    c.last_zero_copy = false;
     auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
     const uint64_t pk_bytes = up(n * 32), off_bytes = up((n + 1) * 8), vwords = (n + 63) / 64;
     const uint64_t v_bytes = up(vwords * 8);
-    const uint64_t blob = sm_off[n] - sm_off[0];
+    const uint64_t base = sm_off[0], blob = sm_off[n] - base;
     const uint64_t total = pk_bytes + off_bytes + v_bytes + blob + PV_BLOB_SLACK;
-    int rc = ensure_stage(total, total);
+    const bool pin_sm = pv_is_pinned(sm + base, blob), pin_pk = pv_is_pinned(pk, 32 * n);
+    const bool pin_off = base == 0 && pv_is_pinned(sm_off, 8 * (n + 1));
+    const bool any_pin = pin_sm || pin_pk || pin_off, all_pin = pin_sm && pin_pk && pin_off;
+    const uint64_t sub = pipe_sub();
+    uint64_t np = blob < PV_PIPE_MIN_BLOB ? 1 : std::max<uint64_t>(1, n / sub);
+    np = std::min<uint64_t>(np, PV_PIPE_MAX);
+    hipStream_t s = c.stream;
+    int rc = ensure_stage(all_pin ? 0 : total, total);
     if (rc) return rc;
-    uint8_t* h = g_ctx.h_stage;
-    uint64_t* hoff = reinterpret_cast<uint64_t*>(h + pk_bytes);
-    {  // keys and rebased offsets, in parallel slices for large batches
-        const uint64_t base = sm_off[0];
+    uint8_t* h = c.h_stage;
+    uint8_t* d = c.d_stage;
+    uint64_t* dver = reinterpret_cast<uint64_t*>(d + pk_bytes + off_bytes);
+    uint8_t* dblob = d + pk_bytes + off_bytes + v_bytes;
+    auto finish_piece = [&](uint64_t lo, uint64_t hi) -> int {
+        c.verdict_zeroed = d_out == nullptr;
+        c.keyed_hint = pv_keyed_hint(pk + 32 * lo, hi - lo);
+        c.hint_set = true;
+        const int r = launch(dblob, reinterpret_cast<const uint64_t*>(d + pk_bytes) + lo, hi - lo, d + 32 * lo,
+                             (d_out ? d_out : dver) + lo / 64, s);
+        c.verdict_zeroed = false;
+        c.keyed_hint = false;
+        c.hint_set = false;
+        return r;
+    };
+    if (np == 1 && !any_pin) {
+        // the quota sizes: everything in the device layout in pinned staging, one DMA
+        uint64_t* hoff = reinterpret_cast<uint64_t*>(h + pk_bytes);
         const unsigned k = n >= (1u << 16) ? 8u : 1u;
-        g_copy_pool.run(k, [&](unsigned t) {
+        cur_pool().run(k, [&](unsigned t) {
             const uint64_t a = n * t / k, b = n * (t + 1) / k;
             memcpy(h + 32 * a, pk + 32 * a, 32 * (b - a));
             for (uint64_t i = a; i < b; i++) hoff[i] = sm_off[i] - base;
         });
         hoff[n] = sm_off[n] - base;
-    }
-    uint8_t* hblob = h + pk_bytes + off_bytes + v_bytes;
-    memset(hblob + blob, 0, PV_BLOB_SLACK);
-    uint8_t* d = g_ctx.d_stage;
-    uint8_t* dblob = d + pk_bytes + off_bytes + v_bytes;
-    hipStream_t s = g_ctx.stream;
-    // the verdict words travel zeroed (the latency path ORs its bits into them)
-    memset(h + pk_bytes + off_bytes, 0, v_bytes);
-    if (blob < (256ull << 10)) {
-        // small batch (Plenum's quotas): one copy of the whole staging area, one DMA
-        memcpy(hblob, sm + sm_off[0], blob);
-        PV_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-    } else if (blob < (8ull << 20)) {
-        // medium: the blob staged by the copy pool, then one DMA of the whole staging area
-        rc = pv_stage_to_device(dblob, hblob, sm + sm_off[0], blob, s, false);
-        if (rc) return rc;
-        PV_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-    } else {
-        PV_HIP(hipMemcpyAsync(d, h, pk_bytes + off_bytes + v_bytes, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-        PV_HIP(hipMemcpyAsync(dblob + blob, hblob + blob, PV_BLOB_SLACK, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
-        rc = pv_stage_to_device(dblob, hblob, sm + sm_off[0], blob, s, true);
-        if (rc) {
-            (void)hipStreamSynchronize(s);  // no DMA may still read the staging buffer when the caller retries
-            return rc;
+        uint8_t* hblob = h + pk_bytes + off_bytes + v_bytes;
+        memset(h + pk_bytes + off_bytes, 0, v_bytes);  // the verdict words travel zeroed
+        memset(hblob + blob, 0, PV_BLOB_SLACK);
+        if (c.inject_stage > 0) {
+            c.inject_stage--;
+            return fail(PV_ERR_ALLOC, "stage_and_launch: injected staging failure (pv_test_inject)");
         }
+        if (blob < (256ull << 10)) {
+            memcpy(hblob, sm + base, blob);
+        } else {
+            rc = pv_stage_to_device(dblob, hblob, sm + base, blob, s, false);
+            if (rc) return rc;
+        }
+        PV_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, s), PV_ERR_LAUNCH);
+        if ((rc = finish_piece(0, n))) return rc;
+        *dver_out = dver;
+        *hver_out = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
+        return PV_OK;
     }
-    uint64_t* dver = reinterpret_cast<uint64_t*>(d + pk_bytes + off_bytes);
-    g_ctx.verdict_zeroed = d_out == nullptr;
-    g_ctx.keyed_hint = pv_keyed_hint(pk, n);
-    g_ctx.hint_set = true;
-    rc = launch(d + pk_bytes + off_bytes + v_bytes, reinterpret_cast<const uint64_t*>(d + pk_bytes), n, d,
-                d_out ? d_out : dver, s);
-    g_ctx.verdict_zeroed = false;
-    g_ctx.keyed_hint = false;
-    g_ctx.hint_set = false;
-    if (rc) return rc;
+    if ((rc = ensure_hver(v_bytes))) return rc;
+    while (c.ev_copy.size() < np) {
+        hipEvent_t e;
+        PV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), PV_ERR_LAUNCH);
+        c.ev_copy.push_back(e);
+    }
+    hipStream_t cs = c.cstream;
+    const uint8_t* spk = pin_pk ? pk : h;
+    const uint64_t* soff = pin_off ? sm_off : reinterpret_cast<const uint64_t*>(h + pk_bytes);
+    const uint8_t* sblob = pin_sm ? sm + base : h + pk_bytes + off_bytes + v_bytes;
+    uint64_t* hoff = reinterpret_cast<uint64_t*>(h + pk_bytes);
+    uint8_t* hblob = h + pk_bytes + off_bytes + v_bytes;
+    uint64_t* doff = reinterpret_cast<uint64_t*>(d + pk_bytes);
+    // the copy stream starts after everything enqueued so far (the previous users of the staging area)
+    PV_HIP(hipEventRecord(c.ev_cstart, s), PV_ERR_LAUNCH);
+    PV_HIP(hipStreamWaitEvent(cs, c.ev_cstart, 0), PV_ERR_LAUNCH);
+    if (c.last_stream && c.last_stream != s) PV_HIP(hipStreamWaitEvent(cs, c.ev_launch_done, 0), PV_ERR_LAUNCH);
+    // sub-batch j = requests [lo(j), lo(j + 1)), 64-aligned bounds
+    auto lo_of = [&](uint64_t j) -> uint64_t { return j == 0 ? 0 : j >= np ? n : (n * j / np) & ~63ull; };
+    pvhost::CopyPool& pool = cur_pool();
+    // sub-batch j's pageable inputs into pinned staging (copy workers), its H2D on the copy stream, then
+    // ev_copy[j]
+    auto stage_copy = [&](uint64_t j) -> int {
+        const uint64_t lo = lo_of(j), hi = lo_of(j + 1);
+        const uint64_t b0 = sm_off[lo] - base, b1 = sm_off[hi] - base;
+        if (!all_pin) {  // this sub-batch's pageable inputs into pinned staging, on the copy workers
+            const unsigned k = std::max(1u, std::min(pool.threads(), (unsigned)((b1 - b0) >> 22)));
+            pool.run(k, [&](unsigned t) {
+                const uint64_t a = lo + (hi - lo) * t / k, b = lo + (hi - lo) * (t + 1) / k;
+                if (!pin_pk) memcpy(h + 32 * a, pk + 32 * a, 32 * (b - a));
+                if (!pin_off)
+                    for (uint64_t i = a; i < b; i++) hoff[i] = sm_off[i] - base;
+                if (!pin_sm) memcpy(hblob + (sm_off[a] - base), sm + sm_off[a], sm_off[b] - sm_off[a]);
+            });
+            if (!pin_off) hoff[hi] = sm_off[hi] - base;
+        }
+        PV_HIP(hipMemcpyAsync(d + 32 * lo, spk + 32 * lo, 32 * (hi - lo), hipMemcpyHostToDevice, cs), PV_ERR_LAUNCH);
+        PV_HIP(hipMemcpyAsync(doff + lo, soff + lo, 8 * (hi - lo + 1), hipMemcpyHostToDevice, cs), PV_ERR_LAUNCH);
+        if (b1 > b0)
+            PV_HIP(hipMemcpyAsync(dblob + b0, sblob + b0, b1 - b0, hipMemcpyHostToDevice, cs), PV_ERR_LAUNCH);
+        PV_HIP(hipEventRecord(c.ev_copy[j], cs), PV_ERR_LAUNCH);
+        return PV_OK;
+    };
+    // PV_PIPE_TRACE=1 (development): timing events after each sub-batch's copies and kernels, printed to
+    // stderr relative to the call's first event -- the untraced pipeline timeline
+    static const bool ptrace = env_int("PV_PIPE_TRACE", 0) != 0;
+    static const int lookahead = env_int("PV_PIPE_LOOKAHEAD", 1);
+    std::vector<hipEvent_t> tev;
+    auto tmark = [&](hipStream_t st) {
+        if (!ptrace) return;
+        hipEvent_t e;
+        if (hipEventCreate(&e) == hipSuccess) {
+            (void)hipEventRecord(e, st);
+            tev.push_back(e);
+        }
+    };
+    // the sub-batches share one set of comb tables: sub-batch 0 builds them, the later ones read them
+    // (the node-side key cache, when it holds keys, plays that role itself)
+    static const bool share_env = env_int("PV_PIPE_SHARE", 1) != 0;
+    const bool share = share_env && np > 1 && (c.path == PV_PATH_AUTO || c.path == PV_PATH_COMB) &&
+                       kc_view().hmask == 0 && ensure_xtab() == PV_OK;
+    auto run = [&]() -> int {
+        tmark(cs);
+        if (share) PV_HIP(hipMemsetAsync(c.xt.htab, 0xFF, PV_XT_HASH * 4, s), PV_ERR_LAUNCH);
+        if (!d_out) PV_HIP(hipMemsetAsync(dver, 0, vwords * 8, s), PV_ERR_LAUNCH);  // the latency path ORs bits
+        PV_HIP(hipMemsetAsync(dblob + blob, 0, PV_BLOB_SLACK, cs), PV_ERR_LAUNCH);
+        int r = stage_copy(0);
+        tmark(cs);
+        // sub-batch j + 1's copies are enqueued BEFORE sub-batch j's kernels: should the copy stream share a
+        // hardware queue with one of the engine's streams, no copy waits behind kernels enqueued before it
+        for (uint64_t j = 0; j < np && r == PV_OK; j++) {
+            if (lookahead && j + 1 < np) {
+                if ((r = stage_copy(j + 1)) != PV_OK) break;
+                tmark(cs);
+            }
+            if (c.inject_stage > 0 && j == std::min<uint64_t>(1, np - 1)) {  // sub-batch 0's kernels in flight
+                c.inject_stage--;
+                return fail(PV_ERR_ALLOC, "stage_and_launch: injected staging failure (pv_test_inject)");
+            }
+            PV_HIP(hipStreamWaitEvent(s, c.ev_copy[j], 0), PV_ERR_LAUNCH);
+            c.xt_fill = share && j == 0;
+            c.xt_use = share && j > 0;
+            r = finish_piece(lo_of(j), lo_of(j + 1));
+            c.xt_fill = c.xt_use = false;
+            tmark(s);
+            if (!lookahead && r == PV_OK && j + 1 < np) {
+                if ((r = stage_copy(j + 1)) != PV_OK) break;
+                tmark(cs);
+            }
+        }
+        return r;
+    };
+    if ((rc = run()) != PV_OK) {
+        (void)hipStreamSynchronize(cs);  // no DMA may still read the caller's or the staging buffers
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
+    if (ptrace && !tev.empty()) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(cs);
+        std::string line = "pv_pipe: n " + std::to_string(n) + " pieces " + std::to_string(np) + " us:";
+        for (size_t i = 1; i < tev.size(); i++) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, tev[0], tev[i]);
+            line += " " + std::to_string((int)(ms * 1000));
+        }
+        fprintf(stderr, "%s\n", line.c_str());
+        for (hipEvent_t e : tev) (void)hipEventDestroy(e);
+    }
     *dver_out = dver;
-    *hver_out = reinterpret_cast<uint64_t*>(h + pk_bytes + off_bytes);
+    *hver_out = c.h_ver;
     return PV_OK;
 }
 
@@ -3529,6 +3737,42 @@ int pv_verify_batch_multi_gpu(const uint8_t* sm, const uint64_t* sm_off, uint64_
         const uint64_t lo = b[r], hi = b[r + 1];
         if (hi > lo) memcpy(verdict_bits + lo / 8, c0.h_mg + (uint64_t)r * wpr, (hi - lo + 7) / 8);
     }
+    return PV_OK;
+}
+
+int pv_host_alloc(void** p, uint64_t bytes) {
+    if (!p) return fail(PV_ERR_ARG, "pv_host_alloc: null pointer");
+    *p = nullptr;
+    void* q = nullptr;
+    PV_HIP(hipHostMalloc(&q, std::max<uint64_t>(bytes, 64), hipHostMallocPortable), PV_ERR_ALLOC);
+    g_pinned_alloc.add(q, std::max<uint64_t>(bytes, 64));
+    *p = q;
+    return PV_OK;
+}
+int pv_host_free(void* p) {
+    if (!p) return PV_OK;
+    if (!g_pinned_alloc.remove(p)) return fail(PV_ERR_ARG, "pv_host_free: not a pv_host_alloc block");
+    PV_HIP(hipHostFree(p), PV_ERR_ALLOC);
+    return PV_OK;
+}
+int pv_host_register(void* p, uint64_t bytes) {
+    if (!p || bytes == 0) return fail(PV_ERR_ARG, "pv_host_register: empty range");
+    PV_HIP(hipHostRegister(p, bytes, hipHostRegisterPortable), PV_ERR_ALLOC);
+    g_pinned_reg.add(p, bytes);
+    return PV_OK;
+}
+int pv_host_unregister(void* p) {
+    if (!g_pinned_reg.remove(p)) return fail(PV_ERR_ARG, "pv_host_unregister: not a registered range");
+    PV_HIP(hipHostUnregister(p), PV_ERR_ALLOC);
+    return PV_OK;
+}
+int pv_host_is_pinned(const void* p, uint64_t bytes) { return pv_is_pinned(p, bytes) ? 1 : 0; }
+
+int pv_test_inject(int what, int device, int count) {
+    if (what != PV_INJECT_STAGE) return fail(PV_ERR_ARG, "pv_test_inject: unknown fault");
+    if (device < 0 || device >= PV_MAX_DEV || count < 0) return fail(PV_ERR_ARG, "pv_test_inject: bad device / count");
+    std::lock_guard<std::mutex> lk(g_mus[device]);
+    g_ctxs[device].inject_stage = count;
     return PV_OK;
 }
 

@@ -7,6 +7,7 @@ If the library is missing, or no gfx950 GPU is visible, verification calls raise
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -84,6 +85,12 @@ SIGNATURES = {
                                                  ctypes.c_void_p]),
     "pv_multi_gpu_devices": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "pv_shard_plan": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, _c_u64p, _c_u64p]),
+    "pv_host_alloc": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint64]),
+    "pv_host_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "pv_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "pv_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
+    "pv_host_is_pinned": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "pv_test_inject": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "pv_stream_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "pv_stream_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_stream_sync": (ctypes.c_int, [ctypes.c_void_p]),
@@ -204,6 +211,51 @@ def verify_sm_batch(blob, offsets, pks):
     if rc:
         check(rc, "pv_verify_batch")
     return np.unpackbits(bits, count=n, bitorder="little").view(bool)
+
+
+PV_INJECT_STAGE = 1  # pv_test_inject: fail the next host-buffer stagings of a device
+
+
+class HostArena:
+    """numpy arrays in the library's pinned host memory (pv_host_alloc). pv_verify_batch /
+    pv_verify_batch_multi_gpu DMA inputs that live there straight to HBM (no pageable -> pinned
+    staging copy): a node that receives its requests into such buffers, or builds its batch there,
+    feeds the GPUs at PCIe rate. The block is freed when the last array viewing it is collected."""
+
+    @staticmethod
+    def empty(shape, dtype=np.uint8):
+        dtype = np.dtype(dtype)
+        count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+        nbytes = max(1, count * dtype.itemsize)
+        p = ctypes.c_void_p()
+        check(lib().pv_host_alloc(ctypes.byref(p), nbytes), "pv_host_alloc")
+        buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+        weakref.finalize(buf, lib().pv_host_free, p.value)
+        return np.frombuffer(buf, dtype=np.uint8, count=count * dtype.itemsize).view(dtype).reshape(shape)
+
+    @staticmethod
+    def is_pinned(arr):
+        arr = np.asarray(arr)
+        return bool(lib().pv_host_is_pinned(arr.ctypes.data, arr.nbytes))
+
+    @classmethod
+    def batch(cls, blob, offsets, pks):
+        """(blob, offsets, pks) copied into arena arrays, offsets rebased to 0 (the form whose offsets
+        are DMA'd as they are)."""
+        offsets = np.asarray(offsets, dtype=np.uint64)
+        base, end = int(offsets[0]), int(offsets[-1])
+        b = cls.empty(max(1, end - base))
+        b[:end - base] = np.asarray(blob, np.uint8)[base:end]
+        o = cls.empty(offsets.shape, np.uint64)
+        np.subtract(offsets, np.uint64(base), out=o)
+        k = cls.empty((len(offsets) - 1, 32))
+        k[:] = np.asarray(pks, np.uint8).reshape(-1, 32)
+        return b, o, k
+
+
+def inject_stage_failures(device, count):
+    """Test hook: the next `count` host-buffer stagings on `device` fail (pv_test_inject)."""
+    check(lib().pv_test_inject(PV_INJECT_STAGE, int(device), int(count)), "pv_test_inject")
 
 
 def comb_fused():

@@ -176,17 +176,27 @@ def test_comb_slot_ranges_at_every_tile_and_xcd_offset(native, sodium):
     within a 256-slot tile and within a round of 8 tiles over the 8 XCDs (the mapping the dropped
     work-queue variant of comb_a got wrong with a period of 2,048 requests). Positions inside each key
     alternate valid / tampered records, so a request verified with another slot's digits or point
-    gets the wrong verdict. AUTO (every key a comb key) and forced COMB, bit-exact."""
+    gets the wrong verdict. AUTO (every key a comb key) and forced COMB, bit-exact. Device-resident
+    inputs (pv_verify_batch_device): the whole batch is ONE launch chunk (a host-buffer call of this
+    size is cut into pipelined sub-batches)."""
+    from bench import DeviceBatch, bits
     blob, off, pks, want = _keyed_records(sodium, 2048, 257, seed=77)
     n = len(off) - 1
     assert n == 2048 * 257
-    for path in (native.PV_PATH_AUTO, native.PV_PATH_COMB):
-        native.set_path(path)
-        got = native.verify_sm_batch(blob, off, pks)
-        split = native.last_split()
-        native.set_path(native.PV_PATH_AUTO)
-        assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
-        assert split == (2048, 2048, n), (path, split)
+    db = DeviceBatch(blob, off, pks)
+    try:
+        for path in (native.PV_PATH_AUTO, native.PV_PATH_COMB):
+            native.set_path(path)
+            db.verify()
+            got = bits(db.verdict_words(), n)
+            split = native.last_split()
+            native.set_path(native.PV_PATH_AUTO)
+            assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
+            assert split == (2048, 2048, n), (path, split)
+    finally:
+        db.free()
+    # the same batch from host buffers (pipelined sub-batches: each a keyed chunk of its own)
+    assert np.array_equal(native.verify_sm_batch(blob, off, pks), want)
 
 
 def test_dedup_lds_table_overflow(native, sodium):

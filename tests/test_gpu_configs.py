@@ -41,19 +41,32 @@ def test_config3_1M_adversarial_bit_exact(native, nym1m, oracle):
     blob2, pks2, idx, labels = inject(blob, off, pks, 0.02, seed=3, oracle=oracle)
     want = cpu_verdicts(blob2, off, pks2)
     # both arithmetic paths: the per-request Straus path and the keyed comb path (~10k distinct
-    # keys here: the 1,024 signers plus every mutated key)
-    for path in (native.PV_PATH_STRAUS, native.PV_PATH_COMB, native.PV_PATH_AUTO):
+    # keys here: the 1,024 signers plus every mutated key). Device-resident, the batch is ONE launch
+    # chunk (the fused comb kernel for AUTO / COMB); from host buffers it runs as pipelined
+    # sub-batches of 131,072 requests, each a chunk of its own
+    from bench import DeviceBatch, bits
+    db = DeviceBatch(blob2, off, pks2)
+    try:
+        for path in (native.PV_PATH_STRAUS, native.PV_PATH_COMB, native.PV_PATH_AUTO):
+            native.set_path(path)
+            db.verify()
+            got = bits(db.verdict_words(), len(want))
+            split = native.last_split()
+            native.set_path(native.PV_PATH_AUTO)
+            assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
+            if path == native.PV_PATH_AUTO:
+                # the 1,024 signers get comb tables; the adversarial one-request keys take the Straus
+                # path in the same launch
+                # (plus the few adversarial keys that recur: blacklisted / non-canonical encodings)
+                assert 1024 <= split[1] < 1200 and split[0] > split[1], split
+                assert len(got) - 30000 < split[2] < len(got), split
+    finally:
+        db.free()
+    for path in (native.PV_PATH_STRAUS, native.PV_PATH_AUTO):
         native.set_path(path)
         got = native.verify_sm_batch(blob2, off, pks2)
-        split = native.last_split()
         native.set_path(native.PV_PATH_AUTO)
-        assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
-        if path == native.PV_PATH_AUTO:
-            # the 1,024 signers get comb tables; the adversarial one-request keys take the Straus
-            # path in the same launch
-            # (plus the few adversarial keys that recur: blacklisted / non-canonical encodings)
-            assert 1024 <= split[1] < 1200 and split[0] > split[1], split
-            assert len(got) - 30000 < split[2] < len(got), split
+        assert np.array_equal(got, want), ("host", path, np.nonzero(got != want)[0][:10])
     # the untouched 98 % are valid and the mutated records are (almost all) rejected
     mask = np.ones(len(got), bool)
     mask[idx] = False
