@@ -288,6 +288,7 @@ PV_HD void pv_comb_a_step(ge_p1p1& t, const ge_p3& acc, const AStage& st, const 
     fe_mul(a, tt, ymx);
     fe_add(tt, acc.Y, acc.X);
     fe_mul(b, tt, ypx);
+    const bool aff = st.affine();  // an affine entry (pv_comb_row_to_affine): Z2 = 2, words 20..27 not fetched
     st.staged(1, w);
 #pragma unroll
     for (int q = 0; q < 10; q++) {
@@ -300,7 +301,12 @@ PV_HD void pv_comb_a_step(ge_p1p1& t, const ge_p3& acc, const AStage& st, const 
     }
     fe_cneg(t2d, t2d, neg);
     fe_mul(c, acc.T, t2d);
-    fe_mul(d, acc.Z, z2);
+    if (aff) {
+        fe_add(d, acc.Z, acc.Z);
+        fe_carry(d, d);
+    } else {
+        fe_mul(d, acc.Z, z2);
+    }
     fe_sub(t.X, b, a);
     fe_add(t.Y, b, a);
     fe_add(t.Z, d, c);
@@ -325,13 +331,70 @@ PV_HD void pv_comb_a_xyz_staged(fe& X, fe& Y, fe& Z, const ge_p3& accB, const AS
     ge_p1p1_to_p2(X, Y, Z, t);
 }
 
+// ---------------------------------------------------------------- affine per-key rows
+// The node-side key cache also keeps each cached key's rows with every entry divided by its Z: in
+// the cached-form layout (40 words: Y+X, Y-X, Z2, 2dT), entry = (y+x, y-x, -, 2dxy). An addition from
+// such an entry needs no Z1 Z2 product (Z2 = 2: D = 2 Z1 is an addition) and does not fetch words
+// 20..27 (pv_comb_a_step with st.affine()): 7 multiplications and 128 B instead of 8 and 160 B.
+// pv_comb_row_to_affine converts one 129-entry cached-form row (src.load(d, c)) with ONE inversion
+// (Montgomery's trick): the running products of the Z2 are parked in words 20..29 of output entry d
+// (dst.e(d): 40 words) until the backward pass has used them. Cached Z2 = 2 Z, so 1/Z = 2 / Z2.
+template <class Src, class Dst>
+PV_HD void pv_comb_row_to_affine(const Src& src, const Dst& dst) {
+    fe prod;
+    fe_1(prod);
+    for (int d = 0; d < PV_COMB_ENT; d++) {
+        ge_cached c;
+        src.load(d, c);
+        fe_mul(prod, prod, c.Z2);
+        uint32_t* e = dst.e(d);
+#pragma unroll
+        for (int q = 0; q < 10; q++) e[20 + q] = prod.v[q];
+    }
+    fe inv;
+    fe_invert(inv, prod);
+    for (int d = PV_COMB_ENT - 1; d >= 0; d--) {
+        ge_cached c;
+        src.load(d, c);
+        fe zi, zi2, t, ypx, ymx, xy2d;
+        if (d > 0) {
+            const uint32_t* p = dst.e(d - 1);
+            fe prev;
+#pragma unroll
+            for (int q = 0; q < 10; q++) prev.v[q] = p[20 + q];
+            fe_mul(zi, inv, prev);  // 1 / Z2_d
+        } else {
+            fe_copy(zi, inv);
+        }
+        fe_mul(inv, inv, c.Z2);
+        fe_add(t, zi, zi);  // 1 / Z_d
+        fe_carry(zi2, t);
+        fe_mul(t, c.YplusX, zi2);
+        fe_canonical(ypx, t);
+        fe_mul(t, c.YminusX, zi2);
+        fe_canonical(ymx, t);
+        fe_mul(t, c.T2d, zi2);
+        fe_canonical(xy2d, t);
+        uint32_t* e = dst.e(d);
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            e[q] = ypx.v[q];
+            e[10 + q] = ymx.v[q];
+            e[20 + q] = 0;
+            e[30 + q] = xy2d.v[q];
+        }
+    }
+}
+
 // Staging over plain Rows objects (host tests): stage() remembers the entry, staged() reads it.
 template <class ARows>
 struct PvRowsStageA {
     const ARows& rows;
     mutable int row_i, ent;
+    bool aff = false;  // rows from pv_comb_row_to_affine
     PV_HD void stage(int i, int d) const { row_i = i; ent = d; }
     PV_HD void staged(int h, uint32_t w[20]) const { rows.row(row_i).load_half(ent, h, w); }
+    PV_HD bool affine() const { return aff; }
 };
 template <class BRows>
 struct PvRowsStageB {

@@ -436,6 +436,7 @@ struct KeyWork {
     uint32_t* comb_cslot;  // [kcap] the same per comb index: its table is read from the cache
     uint32_t* need;        // [PV_ALLCOMB_KEYS][32][5] needed |digit| bits per (comb index, position)
     const uint4* kc_tab;   // the cache's tables [cap][32][129][10] (keycache.h)
+    const uint4* kc_ntab;  // the same divided by Z [cap][32][129][10] (comb.h pv_comb_row_to_affine), or null
     uint32_t hmask;
     uint32_t kcap;
     uint32_t seed;
@@ -469,6 +470,18 @@ __device__ __forceinline__ void pv_glds16_row(const uint4* g, uint4* l) {
                                          (__attribute__((address_space(3))) void*)(l + q * 64 - q), 16, 16 * q, 0);
         pv_glds16_row<Q, q + 1>(g, l);
     }
+}
+// A 10-piece entry whose pieces 5 and 6 (words 20..27) are skipped on lanes with `skip` (affine comb rows:
+// their Z2 words are not read). Lanes that skip leave those pieces of their staging column stale.
+__device__ __forceinline__ void pv_glds16_row10_skip56(const uint4* g, uint4* l, bool skip) {
+    pv_glds16_row<5>(g, l);
+    if (!skip) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)(l + 5 * 64 - 5), 16, 16 * 5, 0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)(l + 6 * 64 - 6), 16, 16 * 6, 0);
+    }
+    pv_glds16_row<10, 7>(g, l);
 }
 // the LDS reads of the previous staged entry must be complete before its buffer is refilled
 __device__ __forceinline__ void pv_lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -1325,11 +1338,13 @@ struct DevCombStage {  // per-key comb table rows, entries of 10 uint4
     const uint4* key;  // the key's table [32][129][10]
     uint4* lds;        // this wave's [10][64] staging area
     uint32_t lane;
+    bool aff;          // affine rows (the key cache's pv_comb_row_to_affine form): rows 5, 6 not fetched
     __device__ __forceinline__ void stage(int i, int d) const {
         const uint4* e = key + ((uint32_t)i * PV_COMB_ENT + (uint32_t)d) * 10;
         pv_lds_reads_done();
-        pv_glds16_row<10>(e, lds);
+        pv_glds16_row10_skip56(e, lds, aff);
     }
+    __device__ __forceinline__ bool affine() const { return aff; }
     __device__ __forceinline__ void staged(int h, uint32_t w[20]) const {
 #pragma unroll
         for (int q = 0; q < 5; q++) {
@@ -1605,6 +1620,37 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_kc_scatter_kernel(const uint4* __
         keys[8 * slots[j] + threadIdx.x] = reinterpret_cast<const uint32_t*>(pk)[8 * j + threadIdx.x];
         if (threadIdx.x == 0) flags[slots[j]] = key_flag[j];
     }
+}
+
+// Key cache fill, second part: the affine rows of every slot just filled (one thread per (slot, position):
+// pv_comb_row_to_affine over the 129 cached-form entries, one inversion).
+struct DevCachedRowSrc {
+    const uint4* r;  // [129][10]
+    __device__ __forceinline__ void load(int d, ge_cached& c) const {
+        uint32_t w[40];
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            const uint4 v = r[d * 10 + q];
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+        ge_cached_load_words(c, w);
+    }
+};
+struct DevAffineRowDst {
+    uint4* r;  // [129][10]
+    __device__ __forceinline__ uint32_t* e(int d) const { return reinterpret_cast<uint32_t*>(r + d * 10); }
+};
+__global__ __launch_bounds__(64) void pv_kc_affine_kernel(const uint4* __restrict__ tab,
+                                                          const uint32_t* __restrict__ slots, uint32_t m,
+                                                          uint4* __restrict__ atab) {
+    const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= m * PV_COMB_POS) return;
+    const uint64_t slot = slots[t / PV_COMB_POS], pos = t % PV_COMB_POS;
+    pv_comb_row_to_affine(DevCachedRowSrc{tab + (slot * PV_COMB_POS + pos) * PV_COMB_ENT * 10},
+                          DevAffineRowDst{atab + (slot * PV_COMB_POS + pos) * PV_COMB_ENT * 10});
 }
 
 // Key cache put: the workspace set up for m keys given in order (d_put_pk[j] is comb index j's key):
@@ -1952,7 +1998,10 @@ __device__ __forceinline__ void pv_comb_a_from(const Work& wk, const KeyWork& kw
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     fe X, Y, Z;
 #if PV_COMB_PIPELINE
-    pv_comb_a_xyz_staged(X, Y, Z, acc, DevCombStage{ktab, stg_wave, threadIdx.x & 63u}, dig);
+    // a cached key with affine rows: additions without the Z1 Z2 product (comb.h pv_comb_row_to_affine)
+    const bool aff = cslot != PV_EMPTY && kw.kc_ntab;
+    if (aff) ktab = kw.kc_ntab + (uint64_t)cslot * PV_COMB_POS * PV_COMB_ENT * 10;
+    pv_comb_a_xyz_staged(X, Y, Z, acc, DevCombStage{ktab, stg_wave, threadIdx.x & 63u, aff}, dig);
 #else
     const DevCombRows arows{const_cast<uint4*>(ktab)};
     pv_comb_a_xyz(X, Y, Z, acc, arows, dig);
@@ -2191,6 +2240,7 @@ struct Ctx {
         uint32_t* d_keys = nullptr;
         uint32_t* d_flags = nullptr;
         uint4* d_tab = nullptr;
+        uint4* d_ntab = nullptr;      // the tables with every entry divided by its Z (comb path), or null
         uint8_t* d_put_pk = nullptr;  // keys of one put batch
         uint32_t* d_put_slot = nullptr;
         uint32_t hmask = 0, seed = 0;
@@ -2269,11 +2319,11 @@ PvKeyCacheView kc_view() {
 
 void kc_free() {
     auto& k = g_ctx.kc;
-    for (void* p : {(void*)k.d_htab, (void*)k.d_keys, (void*)k.d_flags, (void*)k.d_tab, (void*)k.d_put_pk,
-                    (void*)k.d_put_slot})
+    for (void* p : {(void*)k.d_htab, (void*)k.d_keys, (void*)k.d_flags, (void*)k.d_tab, (void*)k.d_ntab,
+                    (void*)k.d_put_pk, (void*)k.d_put_slot})
         if (p) (void)hipFree(p);
     k.d_htab = k.d_keys = k.d_flags = k.d_put_slot = nullptr;
-    k.d_tab = nullptr;
+    k.d_tab = k.d_ntab = nullptr;
     k.d_put_pk = nullptr;
     if (k.async_pending && k.ev_async) (void)hipEventSynchronize(k.ev_async);
     k.async_pending = false;
@@ -2463,6 +2513,7 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
         kw.seg_cap = (uint32_t)((((m + 63) / 64) + PV_NSEG - 1) / PV_NSEG * 64);
         kw.lat_choice = dev_choice ? 1u : 0u;
         kw.kc_tab = kc_tab;
+        kw.kc_ntab = g_ctx.xt_use ? nullptr : g_ctx.kc.d_ntab;
         kw.dense_only = 0;
         if (g_ctx.xt_fill) {  // sub-batch 0 of a pipelined host call: its tables go to the shared store, whole
             kw.ctab = g_ctx.xt.tab;
@@ -3156,6 +3207,24 @@ static void kc_auto_count(const uint8_t* pk, uint64_t n, std::vector<uint8_t>& a
 static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk, uint64_t* d_out,
                             uint64_t** dver_out, uint64_t** hver_out);
 
+// sm_off[0..n] non-decreasing (the host-buffer entries refuse anything else before touching the
+// device); large batches are checked in slices on the calling context's copy workers.
+static bool offsets_nondecreasing(const uint64_t* off, uint64_t n) {
+    auto ok = [off](uint64_t a, uint64_t b) {
+        uint64_t bad = 0;
+        for (uint64_t i = a; i < b; i++) bad |= off[i + 1] < off[i];
+        return bad == 0;
+    };
+    if (n < (1u << 17)) return ok(0, n);
+    pvhost::CopyPool& pool = cur_pool();
+    const unsigned k = std::max(1u, pool.threads());
+    std::atomic<bool> good{true};
+    pool.run(k, [&](unsigned t) {
+        if (!ok(n * t / k, n * (t + 1) / k)) good = false;
+    });
+    return good.load();
+}
+
 static bool pv_keyed_hint(const uint8_t* pk, uint64_t n) {
     if (g_ctx.path != PV_PATH_AUTO || n < PV_KEYED_HINT_MIN || n > PV_LATENCY_MAX) return false;
     if (g_ctx.kc.enabled && !g_ctx.kc.index.empty()) return false;
@@ -3187,8 +3256,7 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_verify_batch: call pv_init first");
     if (n == 0) return PV_OK;
     if (!sm || !sm_off || !pk || !verdict_bits) return fail(PV_ERR_ARG, "null pointer");
-    for (uint64_t i = 0; i < n; i++)
-        if (sm_off[i + 1] < sm_off[i]) return fail(PV_ERR_ARG, "sm_off must be non-decreasing");
+    if (!offsets_nondecreasing(sm_off, n)) return fail(PV_ERR_ARG, "sm_off must be non-decreasing");
     std::lock_guard<std::mutex> lk(g_mu);
 #if PV_ZERO_COPY
     {
@@ -3264,7 +3332,7 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
 // it for A/Bs). Sub-batch j's H2D runs on the copy stream while sub-batch j-1's kernels run, so a large
 // host batch costs about its PCIe time plus the last sub-batch's kernels instead of their sum.
 #ifndef PV_PIPE_SUB
-#define PV_PIPE_SUB 131072
+#define PV_PIPE_SUB 262144
 #endif
 static constexpr uint64_t PV_PIPE_MAX = 64;                // sub-batches per call (copy events)
 static constexpr uint64_t PV_PIPE_MIN_BLOB = 8ull << 20;   // smaller blobs: one piece
@@ -3339,8 +3407,25 @@ static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t 
     const bool pin_off = base == 0 && pv_is_pinned(sm_off, 8 * (n + 1));
     const bool any_pin = pin_sm || pin_pk || pin_off, all_pin = pin_sm && pin_pk && pin_off;
     const uint64_t sub = pipe_sub();
-    uint64_t np = blob < PV_PIPE_MIN_BLOB ? 1 : std::max<uint64_t>(1, n / sub);
-    np = std::min<uint64_t>(np, PV_PIPE_MAX);
+    // sub-batch bounds (64-aligned). The call ends one sub-batch's kernels after the last H2D, and
+    // the first sub-batch's kernels (which also build the shared tables) start only after the first
+    // H2D, so with >= 2 full sub-batches the first and the last are half-size
+    // (profiles/r05/host_path: 1M requests, 0.5 + 3 x 1 + 0.5 of 262,144)
+    std::vector<uint64_t> bnd{0};
+    static const bool halves = env_int("PV_PIPE_HALF_ENDS", 1) != 0;
+    if (blob >= PV_PIPE_MIN_BLOB && halves && n >= 3 * sub) {
+        const uint64_t h = sub / 2 / 64 * 64;
+        const uint64_t mid = n - 2 * h;
+        const uint64_t k = std::min<uint64_t>(PV_PIPE_MAX - 2, std::max<uint64_t>(1, (mid + sub / 2) / sub));
+        bnd.push_back(h);
+        for (uint64_t j = 1; j < k; j++) bnd.push_back(h + (mid * j / k) / 64 * 64);
+        bnd.push_back(n - h);
+    } else if (blob >= PV_PIPE_MIN_BLOB) {
+        const uint64_t k = std::min<uint64_t>(PV_PIPE_MAX, std::max<uint64_t>(1, n / sub));
+        for (uint64_t j = 1; j < k; j++) bnd.push_back((n * j / k) & ~63ull);
+    }
+    bnd.push_back(n);
+    const uint64_t np = bnd.size() - 1;
     hipStream_t s = c.stream;
     int rc = ensure_stage(all_pin ? 0 : total, total);
     if (rc) return rc;
@@ -3405,8 +3490,8 @@ static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t 
     PV_HIP(hipEventRecord(c.ev_cstart, s), PV_ERR_LAUNCH);
     PV_HIP(hipStreamWaitEvent(cs, c.ev_cstart, 0), PV_ERR_LAUNCH);
     if (c.last_stream && c.last_stream != s) PV_HIP(hipStreamWaitEvent(cs, c.ev_launch_done, 0), PV_ERR_LAUNCH);
-    // sub-batch j = requests [lo(j), lo(j + 1)), 64-aligned bounds
-    auto lo_of = [&](uint64_t j) -> uint64_t { return j == 0 ? 0 : j >= np ? n : (n * j / np) & ~63ull; };
+    // sub-batch j = requests [lo(j), lo(j + 1))
+    auto lo_of = [&](uint64_t j) -> uint64_t { return bnd[std::min<uint64_t>(j, np)]; };
     pvhost::CopyPool& pool = cur_pool();
     // sub-batch j's pageable inputs into pinned staging (copy workers), its H2D on the copy stream, then
     // ev_copy[j]
@@ -3649,8 +3734,7 @@ int pv_verify_batch_multi_gpu(const uint8_t* sm, const uint64_t* sm_off, uint64_
                               uint8_t* verdict_bits) {
     if (n == 0) return PV_OK;
     if (!sm || !sm_off || !pk || !verdict_bits) return fail(PV_ERR_ARG, "null pointer");
-    for (uint64_t i = 0; i < n; i++)
-        if (sm_off[i + 1] < sm_off[i]) return fail(PV_ERR_ARG, "sm_off must be non-decreasing");
+    if (!offsets_nondecreasing(sm_off, n)) return fail(PV_ERR_ARG, "sm_off must be non-decreasing");
     std::lock_guard<std::mutex> mg(g_mg_mu);
     const int G = (int)g_mg.devs.size();
     if (G == 0) return fail(PV_ERR_NOT_INIT, "pv_verify_batch_multi_gpu: call pv_init_devices first");
@@ -3843,6 +3927,12 @@ int pv_key_cache_configure(uint32_t capacity) {
         return fail(PV_ERR_ALLOC, std::string("pv_key_cache_configure: hipMalloc: ") + hipGetErrorString(e));
     }
     k.h_async_cap = (uint64_t)g_ctx.kw.kcap * 36 + (uint64_t)H * 4;
+    // the affine rows (660 KB per key): optional -- without them cached keys use the cached-form rows
+    static const bool affine = env_int("PV_KC_AFFINE", 1) != 0;
+    if (affine && hipMalloc((void**)&k.d_ntab, per * capacity) != hipSuccess) {
+        (void)hipGetLastError();
+        k.d_ntab = nullptr;
+    }
     k.cap = capacity;
     k.hmask = H - 1;
     k.seed = (uint32_t)std::random_device{}() | 1u;
@@ -3904,6 +3994,11 @@ static int kc_build_tables(const std::vector<std::string>& fresh, const std::vec
         hipLaunchKernelGGL(pv_kc_scatter_kernel, dim3(64, m), dim3(PV_BLOCK), 0, s, kw.ctab, kw.key_flag, k.d_put_pk,
                            k.d_put_slot, m, k.d_tab, k.d_flags, k.d_keys);
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        if (k.d_ntab) {
+            hipLaunchKernelGGL(pv_kc_affine_kernel, dim3((m * PV_COMB_POS + 63) / 64), dim3(64), 0, s, k.d_tab,
+                               k.d_put_slot, m, k.d_ntab);
+            PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        }
         if (!async) PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // bpk / bslot are host locals
         if (batch++ == fail_batch) return fail(PV_ERR_LAUNCH, "pv_key_cache_put: injected failure (PV_TEST_FAIL_KC_PUT_BATCH)");
     }

@@ -215,7 +215,20 @@ const uint32_t* hc_bcomb_table(void) { return host_bcomb().data(); }
 
 // crypto_sign_open through the comb path with [S]B from pv_comb_b_acc_w<16> (the wide comb's code,
 // W = 16) over the radix-65536 host table, [k](-A) from the staged per-key comb.
+struct HostAffineRowDst {
+    uint32_t* r;  // [129][40]
+    uint32_t* e(int d) const { return r + 40 * d; }
+};
+static int sign_open_comb_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t* pk, bool affine);
 int hc_sign_open_comb_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    return sign_open_comb_wide16(sm, smlen, pk, false);
+}
+// The same with the per-key rows converted by pv_comb_row_to_affine (the key cache's affine rows) and
+// [k](-A) from pv_comb_a_xyz_staged in its affine mode (the device comb kernels on a cached key).
+int hc_sign_open_comb_affine16(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    return sign_open_comb_wide16(sm, smlen, pk, true);
+}
+static int sign_open_comb_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t* pk, bool affine) {
     const std::vector<uint32_t>& bcomb = host_bcomb();
     std::vector<uint8_t> buf(smlen + 256, 0);
     memcpy(buf.data(), sm, smlen);
@@ -243,10 +256,17 @@ int hc_sign_open_comb_wide16(const uint8_t* sm, uint64_t smlen, const uint8_t* p
     HostBRows brows{bcomb.data()};
     ge_p3 acc;
     pv_comb_b_acc_w<16>(acc, PvRowsStageB<HostBRows>{brows, 0, 0}, [&](int j) { return fb[j]; });
-    HostCombRows arows{ctab.data()};
+    std::vector<uint32_t> atab;
+    if (affine) {
+        atab.resize(ctab.size());
+        for (int pos = 0; pos < PV_COMB_POS; pos++)
+            pv_comb_row_to_affine(HostCombRow{ctab.data() + (size_t)pos * PV_COMB_ENT * 40},
+                                  HostAffineRowDst{atab.data() + (size_t)pos * PV_COMB_ENT * 40});
+    }
+    HostCombRows arows{affine ? atab.data() : ctab.data()};
     fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
     bool use[PV_ENC_BATCH];
-    pv_comb_a_xyz_staged(X[0], Y[0], Z[0], acc, PvRowsStageA<HostCombRows>{arows, 0, 0}, dig);
+    pv_comb_a_xyz_staged(X[0], Y[0], Z[0], acc, PvRowsStageA<HostCombRows>{arows, 0, 0, affine}, dig);
     use[0] = ok;
     for (int t = 1; t < PV_ENC_BATCH; t++) { X[t] = X[0]; Y[t] = Y[0]; Z[t] = Z[0]; use[t] = false; }
     uint32_t enc[PV_ENC_BATCH][8];

@@ -300,6 +300,23 @@ def test_wide_comb_path_vs_libsodium(hc, sodium, oracle):
             assert bool(hc.hc_sign_open_comb_wide16(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
 
 
+def test_affine_cached_rows_vs_libsodium(hc, sodium, oracle):
+    """The key cache's affine rows (comb.h pv_comb_row_to_affine: every entry of a 129-entry row divided
+    by its Z with one batched inversion) and the comb loop's affine mode (D = 2 Z1, no Z1 Z2 product,
+    words 20..27 unread) -- the device path of a cached key in the comb kernels: every golden verdict
+    and every adversarial class against libsodium, under the bound assertions."""
+    from vectors import VectorGen
+    with open(os.path.join(HERE, "golden", "verdicts.json")) as f:
+        for c in json.load(f):
+            sm, pk = bytes.fromhex(c["sm"]), bytes.fromhex(c["pk"])
+            assert bool(hc.hc_sign_open_comb_affine16(sm, ctypes.c_uint64(len(sm)), pk)) == c["ok"], c["cls"]
+    g = VectorGen(sodium, oracle, seed=29)
+    for cls in VectorGen.CLASSES:
+        for _ in range(3):
+            sm, pk = g.make(cls)
+            assert bool(hc.hc_sign_open_comb_affine16(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
+
+
 def test_straus_wide_b_vs_libsodium(hc, sodium, oracle):
     """The Straus path as the device runs it with PV_STRAUS_WIDE_B: the loop over k's radix-16 digits
     with the [j](-A) table only, then one addition of [S]B from pv_comb_b_acc_w -- every golden

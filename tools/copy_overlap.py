@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--calls", type=int, default=2)
     ap.add_argument("--gap-us", type=float, default=500.0)
     ap.add_argument("--events", action="store_true")
+    ap.add_argument("--all-kernels", action="store_true", help="list every kernel, not only the step markers")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     kt = table_with(con, ("kernels",))
@@ -112,7 +113,7 @@ def main():
                                 intersect_len(cs, ks) / 1e3))
         if a.events:
             for e in c:
-                if e[0] == "C" or e[1].startswith(("pv_key_insert", "pv_encode", "pv_comb_a", "pv_unpermute")):
+                if e[0] == "C" or a.all_kernels or e[1].startswith(("pv_key_insert", "pv_encode", "pv_comb_a", "pv_unpermute")):
                     print("  %s %-34s %9.1f %9.1f %8.1f %s" % (e[0], e[1][:34], (e[2] - t0) / 1e3, (e[3] - t0) / 1e3,
                                                           (e[3] - e[2]) / 1e3, "%.1f MB" % (e[4] / 1e6) if e[4] else ""))
 
