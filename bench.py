@@ -448,9 +448,11 @@ def pmc_traffic(kernel):
 
 def pmc_valu_issue(kernel, cus=256):
     """VALU issue rate of `kernel` from the committed PMC summary: wave-instructions (SQ_INSTS_VALU) per
-    CU-cycle over its dispatch under the counters (eff. clock = GRBM_GUI_ACTIVE / dispatch time). A
-    full-rate wave64 VALU instruction holds a 16-lane SIMD for 4 cycles, so 4 SIMDs issue at most
-    ~1 per CU-cycle: a value near 1 means the kernel is bound by instruction issue, not memory."""
+    CU-cycle over its dispatch under the counters (eff. clock = GRBM_GUI_ACTIVE / dispatch time). The
+    ceiling depends on the instruction mix: measured ~2.6 cycles per wave64 VOP2 and
+    ~4.9 per VOP3-class instruction (v_mad_u64_u32, v_mul_lo_u32, v_lshrrev_b64) per SIMD, i.e. ~1.5
+    VOP2 or ~0.8 VOP3 instructions per CU-cycle over 4 SIMDs (profiles/r01_isa_rates_full.jsonl): a
+    value near the mix's ceiling means the kernel is bound by instruction issue, not memory."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
@@ -1073,8 +1075,9 @@ def main():
         # the headline batch, device-resident, with the signers' tables in the node-side cache: the
         # keyed path reads them instead of building them (no key chain / table fill in the step).
         # Reported beside the headline, never as `value` (the headline builds every table per step)
-        ks = max(3, args.steps // 4)
-        db.verify()
+        ks = args.steps
+        for _ in range(max(1, args.warmup)):  # the headline's warm-up: the first steps after the puts run slower
+            db.verify()
         elw, _ = timed(ks, stages=False)
         _, stw = timed(ks)
         result["warm_key_cache"] = {
@@ -1083,7 +1086,8 @@ def main():
             "comb_keys": _native.last_split()[1],
             "verdicts_ok": bool(np.array_equal(bits(db.verdict_words(), n), want_local)),
             "note": "configs[1] batch with the 1,024 signers' comb tables in the node-side key cache "
-                    "(pv_key_cache_put before timing): dedup + per-request kernels only"}
+                    "(pv_key_cache_put before timing; the cache keeps each table's entries divided by Z, so a "
+                    "cached key's additions skip the Z1 Z2 product): dedup + per-request kernels only"}
         _native.KeyCache.configure(0)
         lat["note"] = ("host buffers in / verdict bits out, PCIe included; path 3 = latency (one workgroup "
                        "per request, limb-parallel), 1 = Straus; the tampered headline records are included")

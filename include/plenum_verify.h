@@ -191,12 +191,13 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
  *   PV_PATH_LATENCY per request: one workgroup with limb-parallel arithmetic, every field element
  *                   spread over 10 lanes of a 16-lane row; decompression of A and R in one chain,
  *                   the same half-size split as the Straus path, [k1](+-A) and [k2](-R') (~33 x 4
- *                   doublings + ~33 additions each) on two waves at once -- batches of <= 256
- *                   requests: four waves, each scalar cut again at 2^68 (~17 windows per wave) --
+ *                   doublings + ~33 additions each) on two waves at once -- batches of <= 512
+ *                   requests (PV_LAT4_MAX): four waves, each scalar cut again at 2^68 (~17 windows per wave) --
  *                   [k2 S]B from the radix-65536 fixed-base comb, and the comparison with R' without
  *                   an inversion. A key in the node-side key cache keeps the full k: [k](-A) as 32
  *                   table additions, no doublings. One kernel launch; the fastest path for small
- *                   batches (Plenum's 100 / 1,000-message quotas)
+ *                   batches (Plenum's 100 / 1,000-message quotas). In the comb kernels a cached key's
+ *                   additions read the cache's affine rows (entries divided by Z: no Z1 Z2 product)
  *   PV_PATH_AUTO    (default) batches of <= 2,048 requests take the latency path. From 2,049 to
  *                   4,096 requests AUTO picks by key repeats: the keyed path with >= 3 requests per
  *                   key (and <= 2,048 keys), else the latency path; pv_verify_batch counts the keys
