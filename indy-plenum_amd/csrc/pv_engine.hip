@@ -3419,7 +3419,7 @@ static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t 
         const uint64_t k = std::min<uint64_t>(PV_PIPE_MAX - 2, std::max<uint64_t>(1, (mid + sub / 2) / sub));
         bnd.push_back(h);
         for (uint64_t j = 1; j < k; j++) bnd.push_back(h + (mid * j / k) / 64 * 64);
-        bnd.push_back(n - h);
+        bnd.push_back((n - h) & ~63ull);  // every bound a whole verdict word (n itself need not be)
     } else if (blob >= PV_PIPE_MIN_BLOB) {
         const uint64_t k = std::min<uint64_t>(PV_PIPE_MAX, std::max<uint64_t>(1, n / sub));
         for (uint64_t j = 1; j < k; j++) bnd.push_back((n * j / k) & ~63ull);

@@ -34,16 +34,22 @@ def test_config2_1M_valid(native, nym1m):
     assert got.all()
 
 
-def test_config3_1M_adversarial_bit_exact(native, nym1m, oracle):
+@pytest.fixture(scope="module")
+def adv1m(nym1m, oracle):
+    """configs[2]: the 1M batch with 2 % adversarial records, and libsodium's verdicts."""
     from adversarial import inject
     from oracle.oracle import cpu_verdicts
     blob, off, pks = nym1m
     blob2, pks2, idx, labels = inject(blob, off, pks, 0.02, seed=3, oracle=oracle)
-    want = cpu_verdicts(blob2, off, pks2)
+    return blob2, off, pks2, idx, cpu_verdicts(blob2, off, pks2)
+
+
+def test_config3_1M_adversarial_bit_exact(native, adv1m, oracle):
+    blob2, off, pks2, idx, want = adv1m
     # both arithmetic paths: the per-request Straus path and the keyed comb path (~10k distinct
     # keys here: the 1,024 signers plus every mutated key). Device-resident, the batch is ONE launch
     # chunk (the fused comb kernel for AUTO / COMB); from host buffers it runs as pipelined
-    # sub-batches of 131,072 requests, each a chunk of its own
+    # sub-batches of 262,144 requests that share the first one's comb tables
     from bench import DeviceBatch, bits
     db = DeviceBatch(blob2, off, pks2)
     try:
@@ -76,6 +82,37 @@ def test_config3_1M_adversarial_bit_exact(native, nym1m, oracle):
     sub = idx[:600]
     o = np.array([oracle.sign_open_ok(blob2[off[i]:off[i + 1]].tobytes(), pks2[i].tobytes()) for i in sub])
     assert np.array_equal(o, got[sub])
+
+
+def test_config3_1M_cached_signers_bit_exact(native, adv1m):
+    """configs[2] with the 1,024 signers in the node-side key cache (pv_key_cache_put): a cached
+    signer's requests read the cache's affine rows in the comb kernels (D = 2 Z1, no Z1 Z2 product;
+    comb.h pv_comb_row_to_affine), the adversarial keys are not cached and get tables built in the
+    launch or go Straus. Forced COMB and AUTO, device-resident (one 1M chunk: the fused kernel) and from
+    host buffers (pipelined sub-batches on the cached tables), every verdict equal to libsodium's."""
+    import nym_workload
+    from bench import DeviceBatch, bits
+    blob2, off, pks2, idx, want = adv1m
+    kc = native.KeyCache
+    kc.configure(2048)
+    db = DeviceBatch(blob2, off, pks2)
+    try:
+        kc.put([p["vk"] for p in nym_workload._pool()])
+        assert kc.stats()[0] == 1024
+        for path in (native.PV_PATH_COMB, native.PV_PATH_AUTO):
+            native.set_path(path)
+            db.verify()
+            got = bits(db.verdict_words(), len(want))
+            split = native.last_split()
+            assert np.array_equal(got, want), (path, np.nonzero(got != want)[0][:10])
+            assert split[1] >= 1024, split  # every cached signer is a comb key
+            got = native.verify_sm_batch(blob2, off, pks2)
+            native.set_path(native.PV_PATH_AUTO)
+            assert np.array_equal(got, want), ("host", path, np.nonzero(got != want)[0][:10])
+    finally:
+        native.set_path(native.PV_PATH_AUTO)
+        db.free()
+        kc.configure(0)
 
 
 def test_config4_multisig(native, sodium):
