@@ -467,17 +467,21 @@ static_assert(PV_BC2_TOP_ENT <= PV_BC2_ENT, "top row larger than a full row");
 // Y = y+x + y-x, Z = 2, T = X Y / 2: two products instead of an addition's seven); then P - 1 niels
 // additions, each staging the next position's entry while it multiplies (st.stage / st.staged as in
 // pv_comb_b_acc_staged).
+//
+// total > P (per lane): positions total - 1 .. 0 with the stage / digit objects mapping the extra
+// positions to other niels rows -- a cached key's radix-65536 rows (pv_kc_wide: [k](-A) as 16 more
+// niels additions in the same loop).
 template <int P, class BStage, class Digit>
-PV_HD void pv_comb_b_acc_w(ge_p3& acc, const BStage& st, const Digit& digit) {
-    int f = digit(P - 1);
-    st.stage(P - 1, f < 0 ? -f : f);
+PV_HD void pv_comb_b_acc_w(ge_p3& acc, const BStage& st, const Digit& digit, int total = P) {
+    int f = digit(total - 1);
+    st.stage(total - 1, f < 0 ? -f : f);
     {
         uint32_t w[20];
         st.staged(0, w);
         fe ypx, ymx, h;
         pv_sel_pm(ypx, ymx, w, f < 0);
-        f = digit(P - 2);
-        st.stage(P - 2, f < 0 ? -f : f);
+        f = digit(total - 2);
+        st.stage(total - 2, f < 0 ? -f : f);
         fe_sub(acc.X, ypx, ymx);
         fe_carry(acc.X, acc.X);
         fe_add(acc.Y, ypx, ymx);
@@ -489,7 +493,7 @@ PV_HD void pv_comb_b_acc_w(ge_p3& acc, const BStage& st, const Digit& digit) {
         fe_mul(acc.T, acc.T, h);
     }
     ge_p1p1 t;
-    for (int j = P - 2; j >= 0; j--) {
+    for (int j = total - 2; j >= 0; j--) {
         const bool neg = f < 0;
         uint32_t w[20];
         st.staged(0, w);
@@ -516,6 +520,18 @@ PV_HD void pv_comb_b_acc_w(ge_p3& acc, const BStage& st, const Digit& digit) {
         fe_sub(t.T, d, c);
         ge_niels_p1p1_to_p3(acc, t);
     }
+}
+
+// ---------------------------------------------------------------- wide per-key rows (key cache)
+// A cached key may also hold radix-65536 rows W_A[q][d] = [d 65536^q](-A), q = 0..15, d = 0..32896,
+// affine niels (pv_bc2_build_run's format, 128 B per entry, 67 MB per key): [k](-A) is then 16 niels
+// additions (7 multiplications each) instead of 32 cached ones (8 each, 7 from the affine rows). The
+// digit of position q is built from the radix-256 digits the request already has:
+// d_q = e_{2q} + 256 e_{2q+1}, |d_q| <= 128 + 256 x 128 = 32896 -- no second recoding.
+static constexpr int PV_KW_POS = 16;
+static constexpr uint32_t PV_KW_ENT = 32897;
+PV_HD int pv_kw_digit(uint32_t ek_word, int q) {  // ek_word = radix-256 digit word q >> 1
+    return pv_byte(ek_word, 2 * q) + 256 * pv_byte(ek_word, 2 * q + 1);
 }
 
 // Wide fixed-base comb build, one run of cnt consecutive entries d0 .. d0 + cnt - 1 of the row of

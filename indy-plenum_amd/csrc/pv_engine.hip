@@ -437,6 +437,8 @@ struct KeyWork {
     uint32_t* need;        // [PV_ALLCOMB_KEYS][32][5] needed |digit| bits per (comb index, position)
     const uint4* kc_tab;   // the cache's tables [cap][32][129][10] (keycache.h)
     const uint4* kc_ntab;  // the same divided by Z [cap][32][129][10] (comb.h pv_comb_row_to_affine), or null
+    const uint4* kc_wtab;  // radix-65536 rows of slots < kc_wcap [kc_wcap][16][32897][8] (comb.h PV_KW_*), or null
+    uint32_t kc_wcap;
     uint32_t hmask;
     uint32_t kcap;
     uint32_t seed;
@@ -1801,6 +1803,66 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_comb_digits_kernel(Work wk, KeyWo
     wk.flags[i] = w[8 + Bc2<W>::POS];
 }
 
+// The niels loop of a comb slot over the wide fixed-base rows and, when the slot's key has wide cached
+// rows (wkey != null), over those too: positions 16.. are the fixed base's (row j - 16), 0..15 the
+// key's radix-65536 rows (comb.h PV_KW_*). Same entry format, same LDS staging as DevB2Stage.
+template <uint32_t ENT>
+struct DevBWStage {
+    const uint4* base;  // T_B2
+    const uint4* wkey;  // the key's wide rows [16][PV_KW_ENT][8], or null
+    uint4* lds;
+    uint32_t lane;
+    __device__ __forceinline__ void stage(int j, int d) const {
+        const uint4* e = wkey && j < PV_KW_POS
+                             ? wkey + ((uint64_t)j * PV_KW_ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4)
+                             : base + ((uint64_t)(wkey ? j - PV_KW_POS : j) * ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4);
+        pv_lds_reads_done();
+        pv_glds16_row<PV_BCOMB_STRIDE / 4>(e, lds);
+    }
+    __device__ __forceinline__ void staged(int part, uint32_t w[20]) const {
+#pragma unroll
+        for (int q = 0; q < (part ? 3 : 5); q++) {
+            const uint4 v = lds[(5 * part + q) * 64 + lane];
+            const int lim = part ? 10 : 20;
+            if (4 * q < lim) w[4 * q] = v.x;
+            if (4 * q + 1 < lim) w[4 * q + 1] = v.y;
+            if (4 * q + 2 < lim) w[4 * q + 2] = v.z;
+            if (4 * q + 3 < lim) w[4 * q + 3] = v.w;
+        }
+    }
+};
+// The wide rows of slot i's key (null unless the key is cached with wide rows).
+__device__ __forceinline__ const uint4* pv_kw_rows(const KeyWork& kw, uint32_t i) {
+    if (!kw.kc_wtab) return nullptr;
+    const uint32_t cslot = kw.comb_cslot[kw.skey[i]];
+    return cslot < kw.kc_wcap ? kw.kc_wtab + (uint64_t)cslot * PV_KW_POS * PV_KW_ENT * (PV_BCOMB_STRIDE / 4)
+                              : nullptr;
+}
+// [S]B, plus [k](-A) when wkey: the niels loop over 11 (+ 16) positions (comb.h pv_comb_b_acc_w).
+template <int W>
+__device__ __forceinline__ void pv_comb_bw_acc(ge_p3& acc, const uint4* bcomb, const uint4* wkey, const DevDigits& dig,
+                                               uint4* stg_wave) {
+    constexpr int P = Bc2<W>::POS;
+    pv_comb_b_acc_w<P>(
+        acc, DevBWStage<Bc2<W>::ENT>{bcomb, wkey, stg_wave, threadIdx.x & 63u},
+        [&](int j) {
+            if (wkey && j < PV_KW_POS) return pv_kw_digit(dig.ek(j >> 1), j);
+            return dig.fb(wkey ? j - PV_KW_POS : j);
+        },
+        wkey ? P + PV_KW_POS : P);
+}
+// A slot whose [k](-A) was added in the niels loop: projective Q to q rows 0..29 and the key's flag.
+__device__ __forceinline__ void pv_comb_store_q(const Work& wk, const KeyWork& kw, uint32_t i, const ge_p3& acc) {
+    if (kw.key_flag[kw.skey[i]] == 0) wk.flags[i] = 0;
+    const Soa qs(wk.q, 40, wk.stride);
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        qs.st(q, i, acc.X.v[q]);
+        qs.st(10 + q, i, acc.Y.v[q]);
+        qs.st(20 + q, i, acc.Z.v[q]);
+    }
+}
+
 // Wide fixed-base comb rows (comb.h PV_BC2_*): row j = entries 0..PV_BC2_ENT-1 of [d 2^(W j)] B,
 // 8 uint4 each, LDS-staged like DevBStage; 64-bit entry index (the table is ~10.7 GB at W = 24).
 template <uint32_t ENT>
@@ -1830,9 +1892,11 @@ struct DevB2Stage {
 // positions: one entry conversion + PV_BC2_POS - 1 additions). Needs no per-key data, so it runs on
 // the main stream while the key stream builds the tables. acc (extended, 40 words) goes to q rows
 // 0..39.
+// A slot whose key has wide cached rows gets [k](-A) here too (16 more niels additions): pv_comb_a_kernel
+// then only copies its flag.
 template <int W>
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work wk, const uint4* __restrict__ bcomb,
-                                                                 Gate gate) {
+__global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work wk, KeyWork kw,
+                                                                 const uint4* __restrict__ bcomb, Gate gate) {
     if (!gate.keyed() || gate.off()) return;
     const uint32_t i = blockIdx.x * PV_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
@@ -1840,8 +1904,7 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_comb_b_kernel(uint64_t n, Work
     ge_p3 acc;
     __shared__ uint4 stg[PV_BLOCK / 64][PV_BCOMB_STRIDE / 4][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    pv_comb_b_acc_w<Bc2<W>::POS>(acc, DevB2Stage<Bc2<W>::ENT>{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
-                                 [&](int j) { return dig.fb(j); });
+    pv_comb_bw_acc<W>(acc, bcomb, pv_kw_rows(kw, i), dig, &stg[wv][0][0]);
     const Soa qs(wk.q, 40, wk.stride);
 #pragma unroll
     for (int q = 0; q < 10; q++) {
@@ -1969,6 +2032,32 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_bc2_build_kernel(uint4* __restric
                      min(PV_BC2_RUN, ent - d0));
 }
 
+// Key cache fill, third part: the radix-65536 rows of the slots below wcap (comb.h PV_KW_*), keys
+// [j0, j0 + g) of the put batch: one thread per run of PV_BC2_RUN entries of one row, the row's base
+// [65536^q](-A) = the chain's P_{2q}; pv_bc2_build_run (double-and-add start, P-steps, one inversion
+// per run) writes affine niels entries, the Z products in scratch.
+#ifndef PV_KC_WIDE_KEYS
+#define PV_KC_WIDE_KEYS 1024  // keys that get wide rows (67 MB each)
+#endif
+static constexpr uint32_t PV_KW_GROUP = 64;  // keys per wide build launch (scratch: 1.35 GB)
+static constexpr uint32_t PV_KW_RUNS = (PV_KW_ENT + PV_BC2_RUN - 1) / PV_BC2_RUN;  // runs per row
+__global__ __launch_bounds__(PV_BLOCK) void pv_kc_wide_kernel(KeyWork kw, const uint32_t* __restrict__ slots,
+                                                              uint32_t j0, uint32_t g, uint32_t wcap,
+                                                              uint4* __restrict__ wtab, uint32_t* __restrict__ scr) {
+    const uint32_t t = blockIdx.x * PV_BLOCK + threadIdx.x;
+    const uint32_t per_key = PV_KW_POS * PV_KW_RUNS;
+    if (t >= g * per_key) return;
+    const uint32_t jj = t / per_key, q = (t % per_key) / PV_KW_RUNS, r = t % PV_KW_RUNS;
+    const uint32_t j = j0 + jj, slot = slots[j];
+    if (slot >= wcap) return;
+    ge_p3 P;
+    DevBases{kw.bases + (uint64_t)j * PV_COMB_POS * PV_COMB_PTS * 10}.load(2 * q, 0, P);
+    const uint32_t d0 = r * PV_BC2_RUN;
+    pv_bc2_build_run(DevBc2Row{reinterpret_cast<uint32_t*>(wtab + ((uint64_t)slot * PV_KW_POS + q) * PV_KW_ENT * 8)},
+                     DevBc2Scratch{scr + ((uint64_t)jj * PV_KW_POS + q) * PV_KW_ENT * 10}, P, d0,
+                     min(PV_BC2_RUN, PV_KW_ENT - d0));
+}
+
 // XCD-aware block order. Workgroups are dealt round-robin over the 8 XCDs (block b runs on the XCD
 // of b % 8; MI355X_MICROARCH.md, workgroup dispatch), each XCD with its own 4 MB L2. Slot order is
 // key-sorted, so mapping the blocks of XCD x to ONE contiguous range of slots keeps a key's table
@@ -2058,6 +2147,10 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
     if (!gate.keyed() || gate.off()) return;
     const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
+    if (pv_kw_rows(kw, i)) {  // pv_comb_b_kernel added [k](-A) from the key's wide rows: Q is in q rows 0..29
+        if (kw.key_flag[kw.skey[i]] == 0) wk.flags[i] = 0;
+        return;
+    }
     __shared__ uint4 stg[PV_BLOCK / 64][10][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     pv_comb_a_slot(wk, kw, i, &stg[wv][0][0]);
@@ -2090,9 +2183,12 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kern
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     ge_p3 acc;
-    pv_comb_b_acc_w<Bc2<W>::POS>(acc, DevB2Stage<Bc2<W>::ENT>{bcomb, &stg[wv][0][0], threadIdx.x & 63u},
-                                 [&](int j) { return dig.fb(j); });
-    pv_comb_a_from(wk, kw, i, acc, &stg[wv][0][0]);
+    const uint4* wkey = pv_kw_rows(kw, i);
+    pv_comb_bw_acc<W>(acc, bcomb, wkey, dig, &stg[wv][0][0]);
+    if (wkey)  // [k](-A) came from the key's wide rows in the same loop
+        pv_comb_store_q(wk, kw, i, acc);
+    else
+        pv_comb_a_from(wk, kw, i, acc, &stg[wv][0][0]);
 }
 
 // Kernel 3: encode Q for PV_ENC_BATCH requests per lane with one shared inversion, compare with R,
@@ -2241,6 +2337,9 @@ struct Ctx {
         uint32_t* d_flags = nullptr;
         uint4* d_tab = nullptr;
         uint4* d_ntab = nullptr;      // the tables with every entry divided by its Z (comb path), or null
+        uint4* d_wtab = nullptr;      // radix-65536 niels rows of slots < wcap (comb.h PV_KW_*), or null
+        uint32_t wcap = 0;
+        uint32_t* d_wscr = nullptr;   // Z products of one group of wide-row builds
         uint8_t* d_put_pk = nullptr;  // keys of one put batch
         uint32_t* d_put_slot = nullptr;
         uint32_t hmask = 0, seed = 0;
@@ -2320,10 +2419,11 @@ PvKeyCacheView kc_view() {
 void kc_free() {
     auto& k = g_ctx.kc;
     for (void* p : {(void*)k.d_htab, (void*)k.d_keys, (void*)k.d_flags, (void*)k.d_tab, (void*)k.d_ntab,
-                    (void*)k.d_put_pk, (void*)k.d_put_slot})
+                    (void*)k.d_wtab, (void*)k.d_wscr, (void*)k.d_put_pk, (void*)k.d_put_slot})
         if (p) (void)hipFree(p);
-    k.d_htab = k.d_keys = k.d_flags = k.d_put_slot = nullptr;
-    k.d_tab = k.d_ntab = nullptr;
+    k.d_htab = k.d_keys = k.d_flags = k.d_put_slot = k.d_wscr = nullptr;
+    k.d_tab = k.d_ntab = k.d_wtab = nullptr;
+    k.wcap = 0;
     k.d_put_pk = nullptr;
     if (k.async_pending && k.ev_async) (void)hipEventSynchronize(k.ev_async);
     k.async_pending = false;
@@ -2514,6 +2614,8 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
         kw.lat_choice = dev_choice ? 1u : 0u;
         kw.kc_tab = kc_tab;
         kw.kc_ntab = g_ctx.xt_use ? nullptr : g_ctx.kc.d_ntab;
+        kw.kc_wtab = g_ctx.xt_use ? nullptr : g_ctx.kc.d_wtab;
+        kw.kc_wcap = g_ctx.xt_use ? 0u : g_ctx.kc.wcap;
         kw.dense_only = 0;
         if (g_ctx.xt_fill) {  // sub-batch 0 of a pipelined host call: its tables go to the shared store, whole
             kw.ctab = g_ctx.xt.tab;
@@ -2688,7 +2790,7 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_b_done, 0), PV_ERR_LAUNCH);
 #else
             if (!fused) {  // [S]B while the key stream finishes the tables, then join
-                PV_LAUNCH_BC2(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
+                PV_LAUNCH_BC2(pv_comb_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, g_ctx.d_bc2,
                               gate);
                 PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             }
@@ -3933,6 +4035,20 @@ int pv_key_cache_configure(uint32_t capacity) {
         (void)hipGetLastError();
         k.d_ntab = nullptr;
     }
+    // the wide rows (67 MB per key) for the first min(capacity, PV_KC_WIDE_KEYS) slots: optional
+    {
+        const uint32_t want = std::min<uint32_t>(capacity, (uint32_t)std::max(0, env_int("PV_KC_WIDE_KEYS", PV_KC_WIDE_KEYS)));
+        const uint64_t per_w = (uint64_t)PV_KW_POS * PV_KW_ENT * 128;
+        if (want > 0 && hipMalloc((void**)&k.d_wtab, per_w * want) == hipSuccess &&
+            hipMalloc((void**)&k.d_wscr, (uint64_t)PV_KW_GROUP * PV_KW_POS * PV_KW_ENT * 40) == hipSuccess) {
+            k.wcap = want;
+        } else {
+            (void)hipGetLastError();
+            if (k.d_wtab) (void)hipFree(k.d_wtab);
+            k.d_wtab = nullptr;
+            k.wcap = 0;
+        }
+    }
     k.cap = capacity;
     k.hmask = H - 1;
     k.seed = (uint32_t)std::random_device{}() | 1u;
@@ -3998,6 +4114,17 @@ static int kc_build_tables(const std::vector<std::string>& fresh, const std::vec
             hipLaunchKernelGGL(pv_kc_affine_kernel, dim3((m * PV_COMB_POS + 63) / 64), dim3(64), 0, s, k.d_tab,
                                k.d_put_slot, m, k.d_ntab);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+        }
+        if (k.d_wtab) {
+            bool any = false;
+            for (uint32_t j = 0; j < m && !any; j++) any = bslot[j] < k.wcap;
+            for (uint32_t j0 = 0; any && j0 < m; j0 += PV_KW_GROUP) {
+                const uint32_t g = std::min<uint32_t>(PV_KW_GROUP, m - j0);
+                const uint64_t threads = (uint64_t)g * PV_KW_POS * PV_KW_RUNS;
+                hipLaunchKernelGGL(pv_kc_wide_kernel, dim3((unsigned)((threads + PV_BLOCK - 1) / PV_BLOCK)), dim3(PV_BLOCK),
+                                   0, s, kw, k.d_put_slot, j0, g, k.wcap, k.d_wtab, k.d_wscr);
+                PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            }
         }
         if (!async) PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);  // bpk / bslot are host locals
         if (batch++ == fail_batch) return fail(PV_ERR_LAUNCH, "pv_key_cache_put: injected failure (PV_TEST_FAIL_KC_PUT_BATCH)");

@@ -5,6 +5,7 @@
 #include "verify_core.h"
 #include "btable.h"
 #include "comb.h"
+#include <map>
 #include "lp25519.h"
 #include <string.h>
 #include <algorithm>
@@ -267,6 +268,79 @@ static int sign_open_comb_wide16(const uint8_t* sm, uint64_t smlen, const uint8_
     fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
     bool use[PV_ENC_BATCH];
     pv_comb_a_xyz_staged(X[0], Y[0], Z[0], acc, PvRowsStageA<HostCombRows>{arows, 0, 0, affine}, dig);
+    use[0] = ok;
+    for (int t = 1; t < PV_ENC_BATCH; t++) { X[t] = X[0]; Y[t] = Y[0]; Z[t] = Z[0]; use[t] = false; }
+    uint32_t enc[PV_ENC_BATCH][8];
+    pv_encode_batch(enc, X, Y, Z, use);
+    return use[0] && pv_words_equal(enc[0], in.R);
+}
+
+// crypto_sign_open through the comb path with a key's wide cached rows (comb.h PV_KW_*): the key's
+// radix-65536 rows [d 65536^q](-A), d = 0..32896, built by pv_bc2_build_run from the chain's P_{2q},
+// and ONE niels loop over the 16 fixed-base positions (W = 16 host table) and the key's 16 positions
+// with digits d_q = e_{2q} + 256 e_{2q+1} (pv_comb_b_acc_w with total = 32) -- the device's
+// pv_comb_bw_acc. Wide rows are cached per key (a few seconds to build on the host).
+struct HostBWStage {
+    const HostBRows& brows;
+    const uint32_t* wrows;  // [16][PV_KW_ENT][32]
+    mutable int row_i, ent;
+    void stage(int i, int d) const { row_i = i; ent = d; }
+    void staged(int part, uint32_t w[20]) const {
+        const uint32_t* e = row_i < PV_KW_POS ? wrows + ((size_t)row_i * PV_KW_ENT + ent) * PV_BCOMB_STRIDE
+                                              : brows.base + ((size_t)(row_i - PV_KW_POS) * PV_BCOMB_ENT + ent) * PV_BCOMB_STRIDE;
+        memcpy(w, e + 20 * part, part ? 40 : 80);
+    }
+};
+int hc_sign_open_comb_kw16(const uint8_t* sm, uint64_t smlen, const uint8_t* pk) {
+    static std::map<std::string, std::vector<uint32_t>> wide;  // key -> rows
+    const std::vector<uint32_t>& bcomb = host_bcomb();
+    std::vector<uint8_t> buf(smlen + 256, 0);
+    memcpy(buf.data(), sm, smlen);
+    pv_sig_words in;
+    memcpy(in.R, buf.data(), 32);
+    memcpy(in.S, buf.data() + 32, 32);
+    memcpy(in.A, pk, 32);
+    HostMsg mw{buf.data()};
+    bool ok = pv_sig_ok(in, smlen);
+    ge_p3 negA;
+    ok &= pv_key_ok_negate(negA, in.A);
+    uint32_t k[8];
+    pv_hash_k(k, in, smlen, mw);
+    std::string key(reinterpret_cast<const char*>(pk), 32);
+    auto it = wide.find(key);
+    if (it == wide.end()) {
+        std::vector<ge_p3> bases(PV_COMB_POS * PV_COMB_PTS);
+        pv_comb_chain(HostBases{bases.data()}, negA);
+        std::vector<uint32_t> rows((size_t)PV_KW_POS * PV_KW_ENT * PV_BCOMB_STRIDE);
+        std::vector<std::thread> th;
+        for (int q = 0; q < PV_KW_POS; q++)
+            th.emplace_back([&, q] {
+                std::vector<fe> z(PV_KW_ENT);
+                uint32_t* r = rows.data() + (size_t)q * PV_KW_ENT * PV_BCOMB_STRIDE;
+                for (uint32_t d0 = 0; d0 < PV_KW_ENT; d0 += 64)
+                    pv_bc2_build_run(HostBc2Row{r, 0}, HostBc2Scratch{z.data(), 0}, bases[2 * q * PV_COMB_PTS], d0,
+                                     std::min<uint32_t>(64, PV_KW_ENT - d0));
+            });
+        for (auto& t : th) t.join();
+        it = wide.emplace(key, std::move(rows)).first;
+    }
+    pv_dig_regs dig;
+    sc_recode256(dig.e, k);
+    int32_t fb[16];
+    sc_recode_w<16, 16>(fb, in.S);
+    HostBRows brows{bcomb.data()};
+    ge_p3 acc;
+    pv_comb_b_acc_w<16>(acc, HostBWStage{brows, it->second.data(), 0, 0},
+                        [&](int j) {
+                            if (j < PV_KW_POS) return pv_kw_digit(dig.e[j >> 1], j);
+                            return (int)fb[j - PV_KW_POS];
+                        },
+                        16 + PV_KW_POS);
+    fe X[PV_ENC_BATCH], Y[PV_ENC_BATCH], Z[PV_ENC_BATCH];
+    bool use[PV_ENC_BATCH];
+    X[0] = acc.X;
+    Y[0] = acc.Y;
+    Z[0] = acc.Z;
     use[0] = ok;
     for (int t = 1; t < PV_ENC_BATCH; t++) { X[t] = X[0]; Y[t] = Y[0]; Z[t] = Z[0]; use[t] = false; }
     uint32_t enc[PV_ENC_BATCH][8];

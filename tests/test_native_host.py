@@ -317,6 +317,29 @@ def test_affine_cached_rows_vs_libsodium(hc, sodium, oracle):
             assert bool(hc.hc_sign_open_comb_affine16(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
 
 
+def test_wide_cached_rows_vs_libsodium(hc, sodium, oracle):
+    """A cached key's radix-65536 rows (comb.h PV_KW_*: [d 65536^q](-A), d <= 32896, built with the
+    wide fixed-base comb's pv_bc2_build_run from the chain's P_{2q}) and the niels loop that runs the
+    fixed base's positions and the key's 16 in one pass (digits e_{2q} + 256 e_{2q+1}) -- the device's
+    pv_comb_bw_acc: three keys, each with a valid signature, bit flips in R, S and M, S + L and an
+    empty message, against libsodium, under the bound assertions."""
+    import random
+    rnd = random.Random(31)
+    for _ in range(3):
+        pk, sk = sodium.seed_keypair(bytes(rnd.getrandbits(8) for _ in range(32)))
+        for m in (b"", bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(1, 400)))):
+            sm = sodium.sign_detached(m, sk) + m
+            cases = [sm]
+            for pos in (3, 40, 64 + len(m) // 2 if m else 10):
+                t = bytearray(sm)
+                t[pos % len(t)] ^= 1 << rnd.randrange(8)
+                cases.append(bytes(t))
+            s_big = (int.from_bytes(sm[32:64], "little") + 2 ** 252 + 27742317777372353535851937790883648493)
+            cases.append(sm[:32] + (s_big % 2 ** 256).to_bytes(32, "little") + sm[64:])
+            for c in cases:
+                assert bool(hc.hc_sign_open_comb_kw16(c, ctypes.c_uint64(len(c)), pk)) == sodium.sign_open_ok(c, pk)
+
+
 def test_straus_wide_b_vs_libsodium(hc, sodium, oracle):
     """The Straus path as the device runs it with PV_STRAUS_WIDE_B: the loop over k's radix-16 digits
     with the [j](-A) table only, then one addition of [S]B from pv_comb_b_acc_w -- every golden
