@@ -1085,9 +1085,9 @@ def main():
             "ms_per_step": round(1e3 * elw / ks, 3), "stages_ms": {s: round(v, 4) for s, v in stw.items()},
             "comb_keys": _native.last_split()[1],
             "verdicts_ok": bool(np.array_equal(bits(db.verdict_words(), n), want_local)),
-            "note": "configs[1] batch with the 1,024 signers' comb tables in the node-side key cache "
-                    "(pv_key_cache_put before timing; the cache keeps each table's entries divided by Z, so a "
-                    "cached key's additions skip the Z1 Z2 product): dedup + per-request kernels only"}
+            "note": "configs[1] batch with the 1,024 signers in the node-side key cache (pv_key_cache_put "
+                    "before timing; each cached signer also has radix-65536 rows, so its [k](-A) is 16 niels "
+                    "additions inside [S]B's loop): dedup + per-request kernels only"}
         _native.KeyCache.configure(0)
         lat["note"] = ("host buffers in / verdict bits out, PCIe included; path 3 = latency (one workgroup "
                        "per request, limb-parallel), 1 = Straus; the tampered headline records are included")
