@@ -1085,6 +1085,8 @@ def main():
             "ms_per_step": round(1e3 * elw / ks, 3), "stages_ms": {s: round(v, 4) for s, v in stw.items()},
             "comb_keys": _native.last_split()[1],
             "verdicts_ok": bool(np.array_equal(bits(db.verdict_words(), n), want_local)),
+            # the same batch from host memory with the signers cached (what a node with a warm cache gets)
+            "host_path": {k: v for k, v in host_path_leg(blob, off, pks, want_local).items() if k != "note"},
             "note": "configs[1] batch with the 1,024 signers in the node-side key cache (pv_key_cache_put "
                     "before timing; each cached signer also has radix-65536 rows, so its [k](-A) is 16 niels "
                     "additions inside [S]B's loop): dedup + per-request kernels only"}

@@ -248,8 +248,9 @@ int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* laun
  *   pv_key_cache_stats(size, cap)     keys held / capacity
  *   pv_key_cache_contains(pk)         1 if the 32-byte key is cached
  *   pv_key_cache_auto(min_seen)       automatic admission (0 = off, the default): pv_verify_batch calls
- *                                     of <= 4,096 requests count their keys, and a key seen min_seen
- *                                     times within the counting window (the last ~32k distinct keys) is
+ *                                     of <= 4,096 requests count their keys (larger calls count a sample
+ *                                     of 4,096: one request's key per block of ceil(n / 4,096)), and a key seen
+ *                                     min_seen times within the counting window (the last ~32k distinct keys) is
  *                                     put into the cache right behind that batch on the engine stream
  *                                     -- the call waits only for its own verdicts, the table build
  *                                     (~1 ms) overlaps the caller's next steps and the next launch is

@@ -3302,7 +3302,7 @@ static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* s
 // 0.65 vs 0.92; at 2 requests per key (2,048) the latency path still wins (0.58 vs 0.61). Keys in
 // the node-side key cache make the latency path faster still: no hint while the cache holds keys.
 #ifndef PV_KC_AUTO_MAX_BATCH
-#define PV_KC_AUTO_MAX_BATCH 4096  // automatic admission counts keys of host batches up to this size
+#define PV_KC_AUTO_MAX_BATCH 4096  // automatic admission counts every key of host batches up to this size (a sample above)
 #endif
 static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async);
 static void kc_auto_count(const uint8_t* pk, uint64_t n, std::vector<uint8_t>& admit);
@@ -3722,7 +3722,21 @@ bool pv_spin_verdict_bytes(const uint8_t* vb, uint64_t n) {
 int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s, const uint8_t* vb) {
     auto& k = g_ctx.kc;
     std::vector<uint8_t> admit;
-    if (k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken && n <= PV_KC_AUTO_MAX_BATCH) kc_auto_count(pk, n, admit);
+    if (k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken) {
+        if (n <= PV_KC_AUTO_MAX_BATCH) {
+            kc_auto_count(pk, n, admit);
+        } else {  // a large batch counts a sample: one request's key from each block of ceil(n / 4,096), at a
+                  // hashed position in the block (a fixed stride would alias with periodic signer orders)
+            const uint64_t stride = (n + PV_KC_AUTO_MAX_BATCH - 1) / PV_KC_AUTO_MAX_BATCH;
+            std::vector<uint8_t> sample;
+            sample.reserve(32 * (n / stride + 1));
+            for (uint64_t b = 0, t = 0; b < n; b += stride, t++) {
+                const uint64_t i = b + ((t * 0x9E3779B97F4A7C15ull) >> 40) % std::min(stride, n - b);
+                sample.insert(sample.end(), pk + 32 * i, pk + 32 * i + 32);
+            }
+            kc_auto_count(sample.data(), sample.size() / 32, admit);
+        }
+    }
     if (!admit.empty()) {
         PV_HIP(hipEventRecord(g_ctx.ev_verdict_copied, s), PV_ERR_LAUNCH);
         const std::string err = g_err;

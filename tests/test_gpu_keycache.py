@@ -187,6 +187,37 @@ def test_put_failure_rolls_back(nat, sodium, oracle, monkeypatch):
         kc.contains(keys[0][:31])
 
 
+def test_automatic_admission_large_host_batch(nat):
+    """Automatic admission from a large host batch (a node's pipelined calls): a call above 4,096
+    requests counts a sample of 4,096 of its keys, so the 1,024 signers of a 300k-request batch (~4
+    sampled appearances each) are admitted behind the first call -- cached form, affine and wide rows --
+    and the next calls verify from the cache (no shared per-call tables); verdicts exact throughout."""
+    import nym_workload
+    blob, off, pks = nym_workload.generate(0, 300000)
+    bad = np.random.default_rng(9).choice(len(pks), 150, replace=False)
+    blob = blob.copy()
+    for i in bad:
+        blob[int(off[i]) + 90] ^= 0x10
+    want = np.ones(len(pks), bool)
+    want[bad] = False
+    kc = nat.KeyCache
+    kc.configure(2048)
+    kc.auto(2)
+    nat.set_path(nat.PV_PATH_AUTO)
+    try:
+        a0, _ = kc.auto_stats()
+        assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+        a1, f1 = kc.auto_stats()
+        assert a1 - a0 == 1024 and f1 == 0 and kc.stats()[0] == 1024
+        for _ in range(2):
+            assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+        keys, comb_keys, comb_req = nat.last_split()
+        assert comb_keys == keys == 1024, (keys, comb_keys, comb_req)
+    finally:
+        kc.auto(0)
+        kc.configure(0)
+
+
 def test_automatic_admission(nat, sodium, oracle, monkeypatch):
     """pv_key_cache_auto(2): a key is put into the cache behind the host batch in which it is seen
     for the second time (no manual put); verdicts are libsodium's before, during and after the
