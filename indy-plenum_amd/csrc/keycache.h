@@ -24,6 +24,8 @@ struct PvKeyCacheView {
     const uint4* tab;
     uint32_t hmask;   // 0 when the cache is disabled (htab may then be null)
     uint32_t seed;
+    const uint4* wtab = nullptr;  // radix-65536 niels rows of slots < wcap (comb.h PV_KW_*), or null
+    uint32_t wcap = 0;
 };
 
 __host__ __device__ __forceinline__ uint32_t pv_kc_hash(const uint32_t A[8], uint32_t seed) {

@@ -746,6 +746,16 @@ LP_FN lu lp_bcomb_entry(const LpLane& c, const uint32_t* bcomb, int j, int f) {
     const lu w = lp_sel(c.row0, neg ? kk : kk + 10u, lp_sel(c.row1, neg ? kk + 10u : kk, kk + 20u));
     return lp_gather(e, w);
 }
+// The same for entry |f| of row q of a cached key's radix-65536 rows (comb.h PV_KW_*: niels entries
+// in T_B's format, rows of PV_KW_ENT entries).
+LP_FN lu lp_kw_entry(const LpLane& c, const uint32_t* wrows, int q, int f) {
+    const bool neg = f < 0;
+    const uint32_t d = (uint32_t)(neg ? -f : f);
+    const uint32_t* e = wrows + ((uint64_t)q * PV_KW_ENT + d) * PV_BCOMB_STRIDE;
+    const lu kk = lp_sel(c.kge10, 9u, c.k);
+    const lu w = lp_sel(c.row0, neg ? kk : kk + 10u, lp_sel(c.row1, neg ? kk + 10u : kk, kk + 20u));
+    return lp_gather(e, w);
+}
 LP_FN lu lp_bcomb_fix(const LpLane& c, const lu& raw, int f) {
     lu v = raw;
     if (f < 0) v = lp_sel(c.row2, lp_sub(c, 0u, v), v);

@@ -2411,7 +2411,8 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 PvKeyCacheView kc_view() {
-    PvKeyCacheView v{g_ctx.kc.d_htab, g_ctx.kc.d_keys, g_ctx.kc.d_flags, g_ctx.kc.d_tab, 0u, g_ctx.kc.seed};
+    PvKeyCacheView v{g_ctx.kc.d_htab, g_ctx.kc.d_keys, g_ctx.kc.d_flags, g_ctx.kc.d_tab, 0u, g_ctx.kc.seed,
+                     g_ctx.kc.d_wtab, g_ctx.kc.wcap};
     if (g_ctx.kc.enabled && !g_ctx.kc.broken && g_ctx.kc.cap > 0 && !g_ctx.kc.index.empty()) v.hmask = g_ctx.kc.hmask;
     return v;
 }

@@ -333,13 +333,17 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
     __shared__ uint32_t s_k256[8];          // radix-256 digits of k (cached key)
     __shared__ uint32_t s_sig_ok, s_nw, s_neg;
     __shared__ volatile uint32_t s_pts_ready;  // wave 0 -> waves 2, 3: -A and R' published
+    __shared__ volatile uint32_t s_k_ready;    // cached key: wave 1 -> waves 2, 3: k's digits published
     __shared__ uint32_t s_pa[64], s_pr[64];    // -A, R' (ext)
     __shared__ uint32_t s_part[3][64];         // wave 1, 2, 3 results (cached form)
     __shared__ uint32_t s_fs[8];               // radix-65536 digits of s2 = k2 S mod L (waves 2, 3: [s2]B)
     __shared__ uint32_t s_tab[4][17][64];      // [j] of -A, R', [2^68](-A), [2^68]R', j = -8..8
     __shared__ uint32_t s_msg[ZC ? PV_ZC_MSG_WORDS : 1];
 
-    if (threadIdx.x == 0) s_pts_ready = 0u;
+    if (threadIdx.x == 0) {
+        s_pts_ready = 0u;
+        s_k_ready = 0u;
+    }
     LAT_STAMP(wave == 0 ? 16 : 19);  // kernel entry (19: unused slot for the other waves)
     uint64_t smlen;
     const uint32_t* ap;
@@ -375,10 +379,43 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
     const LpConsts K = LpConsts::make(c);
     const uint32_t slot = __builtin_amdgcn_readfirstlane(pv_kc_lookup(kc, in.A));
     const bool cached = slot != PV_KC_EMPTY;
+    const bool wide = cached && kc.wtab && slot < kc.wcap;  // the key's radix-65536 rows (comb.h PV_KW_*)
     __syncthreads();  // 0: s_pts_ready cleared
     LAT_STAMP(wave == 0 ? 0 : (wave == 1 ? 8 : 14));
 
     if (wave >= 2) {
+        if (cached) {
+            // [k](-A) in two halves beside wave 0's decompression of R (the only point a cached key still
+            // needs): as soon as wave 1 has k's digits, wave 2 adds the upper, wave 3 the lower positions
+            // -- 8 niels entries each from the wide rows, else 16 cached ones
+            while (s_k_ready == 0u) __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            uint32_t e256[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) e256[q] = s_k256[q];
+            lu acc = lp_identity_ext(c);
+            if (wide) {
+                const uint32_t* wr =
+                    reinterpret_cast<const uint32_t*>(kc.wtab + (uint64_t)slot * PV_KW_POS * PV_KW_ENT * (PV_BCOMB_STRIDE / 4));
+                const int q0 = wave == 2 ? PV_KW_POS / 2 : 0;
+                lu ent[PV_KW_POS / 2];
+#pragma unroll
+                for (int jj = 0; jj < PV_KW_POS / 2; jj++) ent[jj] = lp_kw_entry(c, wr, q0 + jj, pv_kw_digit(e256[(q0 + jj) >> 1], q0 + jj));
+#pragma unroll
+                for (int jj = PV_KW_POS / 2 - 1; jj >= 0; jj--)
+                    acc = lp_add_cached(c, acc, lp_bcomb_fix(c, ent[jj], pv_kw_digit(e256[(q0 + jj) >> 1], q0 + jj)));
+            } else {
+                const uint32_t* tab = reinterpret_cast<const uint32_t*>(kc.tab + (uint64_t)slot * PV_COMB_POS * PV_COMB_ENT * 10);
+                const int i0 = wave == 2 ? PV_COMB_POS / 2 : 0;
+                lu ent[PV_COMB_POS / 2];
+#pragma unroll
+                for (int ii = 0; ii < PV_COMB_POS / 2; ii++) ent[ii] = lp_ctab_load(c, tab, i0 + ii, pv_byte(e256[(i0 + ii) >> 2], i0 + ii));
+#pragma unroll
+                for (int ii = PV_COMB_POS / 2 - 1; ii >= 0; ii--)
+                    acc = lp_add_cached(c, acc, lp_ctab_fix(c, ent[ii], pv_byte(e256[(i0 + ii) >> 2], i0 + ii)));
+            }
+            s_part[wave - 1][lane] = lp_to_cached(c, acc, K.d2);
+        }
         if (!cached) {
             // the 68 doublings run on y alone from the encoding (lp_ydbl_chain), beside wave 0's
             // decompression; x enters once it is published
@@ -438,9 +475,12 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
             if (lane == 0) {
 #pragma unroll
                 for (int q = 0; q < 8; q++) s_k256[q] = e256[q];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                s_k_ready = 1u;  // waves 2 and 3 start [k](-A) now, not at barrier 1
             }
-            __syncthreads();  // 1
+            // [S]B also before barrier 1: beside wave 0's decompression, off its chain
             s_part[0][lane] = lp_to_cached(c, lp_comb_b(c, [&](int j) -> lu { return lp_bcomb_fix(c, ent[j], pv_half(fs[j >> 1], j)); }), K.d2);
+            __syncthreads();  // 1
             __syncthreads();  // 2
             return;
         }
@@ -494,17 +534,11 @@ __device__ __forceinline__ void lat4_body(const uint32_t* __restrict__ zsrc, con
     bool key_ok;
     lu QA;
     if (cached) {
+        // waves 2 and 3 built the two halves of [k](-A) during the decompression
         key_ok = kc.flags[slot] != 0;
-        const uint32_t* tab = reinterpret_cast<const uint32_t*>(kc.tab + (uint64_t)slot * PV_COMB_POS * PV_COMB_ENT * 10);
         __syncthreads();  // 1
-        uint32_t e256[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) e256[q] = s_k256[q];
-        lu ent[PV_COMB_POS];
-#pragma unroll
-        for (int i = 0; i < PV_COMB_POS; i++) ent[i] = lp_ctab_load(c, tab, i, pv_byte(e256[i >> 2], i));
-        QA = lp_comb_a(c, [&](int i) { return lp_ctab_fix(c, ent[i], pv_byte(e256[i >> 2], i)); });
         __syncthreads();  // 2
+        QA = lp_add_cached(c, lp_add_cached(c, lp_identity_ext(c), lu(s_part[1][lane])), lu(s_part[2][lane]));
     } else {
         key_ok = pv_ge_is_canonical(in.A) && !pv_has_small_order(in.A) && dec.ok_a;
         const lu negA = lp_ext_from_xy(c, K, dec.X, dec.Y, 0);

@@ -69,6 +69,34 @@ def test_cached_keys_bit_exact(nat, sodium, oracle):
     kc.enable(True)
 
 
+def test_latency_four_wave_cached_forms(nat, sodium, oracle, monkeypatch):
+    """The four-wave latency kernel (<= 512 requests, the zero-copy form Plenum's quotas and singletons
+    take) on cached keys: waves 2 and 3 add the two halves of [k](-A) while wave 0 decompresses R --
+    from the keys' radix-65536 rows (8 niels entries per wave) or, with the wide rows off, from the
+    cached-form table (16 per wave). Single requests, a 33-request and a 300-request batch with
+    cached, uncached and bad (cached, failing key checks) keys: libsodium's verdicts."""
+    cases, keys, bad = _batch(sodium, oracle, seed=57)
+    blob, off, pks = pack(cases)
+    want = _want(sodium, cases)
+    kc = nat.KeyCache
+    nat.set_path(nat.PV_PATH_AUTO)
+    try:
+        for wide in ("1024", "0"):
+            monkeypatch.setenv("PV_KC_WIDE_KEYS", wide)
+            kc.configure(64)
+            kc.put(keys[:30] + bad)
+            for lo, hi in ((0, 1), (7, 8), (40, 73), (100, 400)):
+                o = off[lo:hi + 1]
+                got = nat.verify_sm_batch(blob[:int(o[-1])], o, pks[lo:hi])
+                assert np.array_equal(got, want[lo:hi]), (wide, lo, hi, np.nonzero(got != want[lo:hi])[0][:10])
+            for i in range(0, len(want), 37):  # one-request calls (the slot in the kernel arguments)
+                o = off[i:i + 2]
+                assert bool(nat.verify_sm_batch(blob[:int(o[-1])], o, pks[i:i + 1])[0]) == bool(want[i]), (wide, i)
+    finally:
+        monkeypatch.delenv("PV_KC_WIDE_KEYS", raising=False)
+        kc.configure(0)
+
+
 def test_eviction_and_clear(nat, sodium, oracle):
     cases, keys, bad = _batch(sodium, oracle, seed=52, n=800)
     blob, off, pks = pack(cases)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--sizes", default="262144,1048576")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-arena", action="store_true")
+    ap.add_argument("--cache", type=int, default=0, help="key cache capacity; the 1,024 signers are put before timing")
     args = ap.parse_args()
     sizes = [int(x) for x in args.sizes.split(",")]
     nmax = max(sizes)
@@ -35,6 +36,9 @@ def main():
         blob, off, pks = nym_workload.generate(0, nmax)
     print(json.dumps({"generated": len(off) - 1, "s": round(time.perf_counter() - t0, 2)}), flush=True)
     _native.ensure_device(0)
+    if args.cache:
+        _native.KeyCache.configure(args.cache)
+        _native.KeyCache.put([p["vk"] for p in nym_workload._pool()])
     arena = None
     if not args.no_arena and hasattr(_native, "HostArena"):
         arena = _native.HostArena
