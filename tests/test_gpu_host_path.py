@@ -103,6 +103,26 @@ def test_init_devices_bad_mask_keeps_primary(native, adv400k):
     _check(native.verify_sm_batch_multi(blob[:int(o[-1])], o, pks[:5000]), want[:5000], "multi after bad mask")
 
 
+def test_pipelined_shared_tables_with_one_off_keys(native, sodium):
+    """A pipelined host call whose first sub-batch has more than 2,048 distinct keys (1,024 signers
+    with ~100 requests each plus ~25k one-off keys): the first sub-batch gives tables only to the
+    signers (>= 48 requests) and publishes them; the later sub-batches read the signers' tables from
+    the shared store and verify their one-off keys on the Straus path in the same launches -- forced
+    COMB too (every key a comb key up to the capacity) -- libsodium's verdicts."""
+    from test_gpu_configs import _split_batch
+    from oracle.oracle import cpu_verdicts
+    blob, off, pks = _split_batch(sodium, 262144, 60000, seed=17)
+    want = cpu_verdicts(blob, off, pks)
+    assert 0 < (~want).sum() < len(want) // 50
+    for path in (native.PV_PATH_AUTO, native.PV_PATH_COMB):
+        native.set_path(path)
+        try:
+            got = native.verify_sm_batch(blob, off, pks)
+        finally:
+            native.set_path(native.PV_PATH_AUTO)
+        _check(got, want, ("one-off keys", path))
+
+
 def test_multi_gpu_two_or_more_devices(native, adv400k):
     L = native.lib()
     G = L.pv_device_count()
