@@ -58,9 +58,109 @@ rel_b:
     return PyLong_FromLong(rc);
 }
 
+/* finish_single(verified, results, a, b, keys_hex, sig_lines, sig_off, pair_off, pair_name, names):
+ * plenum_amd/wire.py's per-request finish of device-verified single-signature requests a..b-1, in
+ * request order, as ReqAuthenticator.authenticate leaves them (plenum/server/req_authenticator.py:
+ * 31-50): key = Request.digest (64 hex digits, line i of keys_hex), sig = the signature text (line
+ * pair_off[i] of sig_lines); if verified[key] exists with the same 'signature' its 'identifiers'
+ * are the result, else verified[key] = {'signature': sig, 'identifiers': {identifier}} and that set
+ * is. `verified` must be an exact dict and `results` a list (the caller checks). Exceptions raised
+ * by an existing entry's lookup or comparison propagate, as they do from the Python loop. */
+static PyObject* fc_finish_single(PyObject* self, PyObject* args) {
+    PyObject *verified, *results, *names, *okh, *osl, *oso, *opo, *opn;
+    Py_ssize_t a, b;
+    Py_buffer kh, sl, so, po, pn;
+    PyObject* ret = NULL;
+    PyObject *k_sig = NULL, *k_ids = NULL;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "O!O!nnOOOOOO!", &PyDict_Type, &verified, &PyList_Type, &results, &a, &b, &okh,
+                          &osl, &oso, &opo, &opn, &PyList_Type, &names))
+        return NULL;
+    if (PyObject_GetBuffer(okh, &kh, PyBUF_C_CONTIGUOUS) < 0) return NULL;
+    if (PyObject_GetBuffer(osl, &sl, PyBUF_C_CONTIGUOUS) < 0) goto r_kh;
+    if (PyObject_GetBuffer(oso, &so, PyBUF_C_CONTIGUOUS) < 0) goto r_sl;
+    if (PyObject_GetBuffer(opo, &po, PyBUF_C_CONTIGUOUS) < 0) goto r_so;
+    if (PyObject_GetBuffer(opn, &pn, PyBUF_C_CONTIGUOUS) < 0) goto r_po;
+    {
+        const char* keys = (const char*)kh.buf;
+        const char* lines = (const char*)sl.buf;
+        const uint64_t* soff = (const uint64_t*)so.buf;
+        const uint64_t* poff = (const uint64_t*)po.buf;
+        const uint32_t* pname = (const uint32_t*)pn.buf;
+        const Py_ssize_t n_pairs = so.len / 8 - 1, n_names = PyList_GET_SIZE(names);
+        if (a < 0 || b < a || b > PyList_GET_SIZE(results) || kh.len < 65 * b || po.len < 8 * (b + 1) ||
+            so.len < 8 || so.len % 8 || pn.len < 4 * n_pairs) {
+            PyErr_SetString(PyExc_ValueError, "finish_single: inconsistent plan buffers");
+            goto done;
+        }
+        k_sig = PyUnicode_InternFromString("signature");
+        k_ids = PyUnicode_InternFromString("identifiers");
+        if (!k_sig || !k_ids) goto done;
+        for (Py_ssize_t i = a; i < b; i++) {
+            const Py_ssize_t p = (Py_ssize_t)poff[i];
+            if (p < 0 || p >= n_pairs || pname[p] >= (uint64_t)n_names ||
+                (Py_ssize_t)(soff[p + 1] + p + 1) > sl.len || soff[p + 1] < soff[p]) {
+                PyErr_SetString(PyExc_ValueError, "finish_single: pair index out of range");
+                goto done;
+            }
+            const char* kp = keys + 65 * i;
+            Py_ssize_t kl = 0;
+            while (kl < 64 && kp[kl] != '\n') kl++;
+            PyObject* key = PyUnicode_DecodeASCII(kp, kl, NULL);
+            if (!key) goto done;
+            PyObject* sig = PyUnicode_DecodeASCII(lines + soff[p] + p, (Py_ssize_t)(soff[p + 1] - soff[p]), NULL);
+            if (!sig) { Py_DECREF(key); goto done; }
+            PyObject* seen = PyDict_GetItemWithError(verified, key);  /* borrowed */
+            PyObject* res = NULL;
+            if (seen) {
+                Py_INCREF(seen);
+                PyObject* old = PyObject_GetItem(seen, k_sig);
+                int same = old ? PyObject_RichCompareBool(old, sig, Py_EQ) : -1;
+                Py_XDECREF(old);
+                if (same > 0) res = PyObject_GetItem(seen, k_ids);
+                Py_DECREF(seen);
+                if (same < 0 || (same > 0 && !res)) { Py_DECREF(key); Py_DECREF(sig); goto done; }
+            } else if (PyErr_Occurred()) {
+                Py_DECREF(key); Py_DECREF(sig); goto done;
+            }
+            if (!res) {
+                PyObject* ids = PySet_New(NULL);
+                PyObject* ent = PyDict_New();
+                if (!ids || !ent || PySet_Add(ids, PyList_GET_ITEM(names, pname[p])) < 0 ||
+                    PyDict_SetItem(ent, k_sig, sig) < 0 || PyDict_SetItem(ent, k_ids, ids) < 0 ||
+                    PyDict_SetItem(verified, key, ent) < 0) {
+                    Py_XDECREF(ids); Py_XDECREF(ent); Py_DECREF(key); Py_DECREF(sig); goto done;
+                }
+                Py_DECREF(ent);
+                res = ids;
+            }
+            Py_DECREF(key);
+            Py_DECREF(sig);
+            PyList_SetItem(results, i, res);  /* steals res, releases the previous item */
+        }
+        ret = Py_None;
+        Py_INCREF(ret);
+    }
+done:
+    Py_XDECREF(k_sig);
+    Py_XDECREF(k_ids);
+    PyBuffer_Release(&pn);
+r_po:
+    PyBuffer_Release(&po);
+r_so:
+    PyBuffer_Release(&so);
+r_sl:
+    PyBuffer_Release(&sl);
+r_kh:
+    PyBuffer_Release(&kh);
+    return ret;
+}
+
 static PyMethodDef fc_methods[] = {
     {"bind", fc_bind, METH_VARARGS, "bind(address of pv_verify_batch)"},
     {"verify", fc_verify, METH_VARARGS, "verify(blob, offsets, pks, bits) -> pv_verify_batch's return code"},
+    {"finish_single", fc_finish_single, METH_VARARGS,
+     "finish_single(verified, results, a, b, keys_hex, sig_lines, sig_off, pair_off, pair_name, names)"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef fc_module = {PyModuleDef_HEAD_INIT, "_fastcall", NULL, -1, fc_methods,

@@ -430,7 +430,14 @@ def _authenticate_packed(req_authnr, blob, off, threads, timings, one_call_per_r
             np.cumsum(~good, out=bad[1:])
             fast = cand & (bad[hi] == bad[lo])
     t3 = time.perf_counter()
-    keys_all = P.keys()  # request i's key (Request.digest, hex) when its serialization succeeded
+    verified = req_authnr._verified_reqs
+    fc = _native._fastcall()
+    # the device-verified single-signature requests are finished in C (_fastcall.finish_single: the
+    # same per-request dict operations, without the interpreter) when the cache is a plain dict
+    c_finish = bool(fc) and hasattr(fc, "finish_single") and type(verified) is dict and not one_call_per_request
+    # request i's key (Request.digest, hex) when its serialization succeeded; only the requests that
+    # are not finished in C need it as a str
+    keys_all = P.keys() if not (c_finish and (fast & (P.kind == PV_PLAN_SINGLE)).all()) else None
     ser_ok = (P.status == PV_SER_OK).tolist()
     msgs, other, slow_views = {}, {}, []
     names = P.names
@@ -485,10 +492,9 @@ def _authenticate_packed(req_authnr, blob, off, threads, timings, one_call_per_r
     if one_call_per_request:
         fast[:] = False  # every request takes one authenticate call
     results = [None] * n
-    verified = req_authnr._verified_reqs
     vget = verified.get
     kind = P.kind
-    sigs_all = P.signatures() if fast.any() else []
+    sigs_all = P.signatures() if fast.any() and not c_finish else []
 
     def one(i):  # request i in order, as the sequential path would finish it
         if fast[i]:
@@ -517,7 +523,7 @@ def _authenticate_packed(req_authnr, blob, off, threads, timings, one_call_per_r
             results[i] = ex
 
     simple = fast & (kind == PV_PLAN_SINGLE)
-    if simple.any():
+    if simple.any() and not c_finish:
         # distinct keys among the device-finished requests (a 64-bit prefix suffices to prove it)
         pre = P.digests[simple, :8].copy().view(np.uint64).ravel()
         keys_distinct = np.unique(pre).size == pre.size
@@ -526,6 +532,9 @@ def _authenticate_packed(req_authnr, blob, off, threads, timings, one_call_per_r
         """Requests a..b-1, all device-finished single-signature ones: when their keys are new
         and distinct (the usual batch), the cache entries go in with one dict.update in request
         order — the state the per-request sequence leaves — else one by one."""
+        if c_finish:
+            fc.finish_single(verified, results, a, b, P._keys_hex, P._sig_lines, P.sig_off, po, pn, names)
+            return
         keys = keys_all[a:b]
         if not keys_distinct or not verified.keys().isdisjoint(keys):
             for i in range(a, b):

@@ -227,3 +227,55 @@ def test_wire_batch_one_call_per_request_cpu(cpu_engine, sodium, monkeypatch):
     assert cpu_engine["sm"] == 1  # the plan's one launch; nothing verified one by one
     # device-finished requests were answered from the plan inside the one authenticate call
     assert sum(answered) > 10 and not all(answered)
+
+
+def test_c_finisher_matches_python_finish(cpu_engine, sodium):
+    """_fastcall.finish_single (the C finish of device-verified single-signature requests) leaves
+    the same results and verified-request cache as the Python finish: new keys, a key repeated in
+    the batch, keys already cached with the same signature (the cached identifier set is returned)
+    and with another signature (overwritten), and a second pass over the whole batch."""
+    import nym_workload
+    fc = _native._fastcall()
+    if not fc or not hasattr(fc, "finish_single"):
+        pytest.skip("_fastcall not built (make -C indy-plenum_amd)")
+    k = 3000
+    _, _, _, wblob, woff, _, _ = nym_workload.generate_wire(0, k)
+    pool = nym_workload._pool()
+    raws = [wblob[int(woff[i]):int(woff[i + 1])].tobytes() for i in range(k)]
+    raws[10] = raws[5]   # a key repeated inside the batch
+    raws[2000] = raws[7]
+
+    def make():
+        core = CoreAuthNr(["1"], ["105"], [], state=None)
+        for p in pool:
+            core.addIdr(p["did"], p["abbr"])
+        from plenum_amd.req_authenticator import ReqAuthenticator
+        ra = ReqAuthenticator()
+        ra.register_authenticator(core)
+        return ra
+
+    def run(use_c):
+        calls = []
+        with pytest.MonkeyPatch.context() as mp:
+            if use_c:
+                orig = fc.finish_single
+                mp.setattr(fc, "finish_single", lambda *a: (calls.append(a[2:4]), orig(*a))[1])
+            else:
+                mp.setattr(_native, "_fast", False)
+            ra = make()
+            first = wire.authenticate_wire_batch(ra, raws[:1500])
+            keys = list(ra._verified_reqs)
+            ra._verified_reqs[keys[3]] = {"signature": "other", "identifiers": {"x"}}  # overwritten
+            cached = ra._verified_reqs[keys[4]]["identifiers"]
+            out = wire.authenticate_wire_batch(ra, raws)
+            again = wire.authenticate_wire_batch(ra, raws)
+        return first, out, again, ra._verified_reqs, out[4][1] is cached, calls
+
+    c = run(True)
+    py = run(False)
+    assert c[5] and not py[5]
+    for a, b in zip(c[:3], py[:3]):
+        assert [norm(r) for r in a] == [norm(r) for r in b]
+    assert c[3] == py[3] and list(c[3]) == list(py[3])
+    assert c[4] and py[4]
+    assert all(r == {pool[i % len(pool)]["did"]} for i, (_, r) in enumerate(c[1]) if i not in (10, 2000))
