@@ -153,6 +153,67 @@ class PinnedRegistry {
     std::map<uintptr_t, uint64_t> r_;
 };
 
+// Blocks released by pv_host_free, kept pinned for the next pv_host_alloc of a similar size (a node
+// allocates its receive arenas again and again; a fresh pinned allocation costs ~0.1 s per 400 MB,
+// and one made late in a long-lived process can land on pages the DMA engines read at half rate --
+// profiles/r05/host_path/README.txt). take(bytes) returns the smallest cached block of at least
+// `bytes` and at most twice that, or null; put() keeps a block and returns the blocks the total
+// budget pushes out (oldest first), which the caller frees; drain() returns all of them.
+class PinnedCache {
+   public:
+    struct Block {
+        void* p;
+        uint64_t bytes;
+    };
+    explicit PinnedCache(uint64_t budget) : budget_(budget) {}
+    Block take(uint64_t bytes) {
+        std::lock_guard<std::mutex> lk(mu_);
+        size_t best = blocks_.size();
+        for (size_t i = 0; i < blocks_.size(); i++) {
+            const uint64_t b = blocks_[i].bytes;
+            if (b >= bytes && b / 2 <= bytes && (best == blocks_.size() || b < blocks_[best].bytes)) best = i;
+        }
+        if (best == blocks_.size()) return {nullptr, 0};
+        const Block r = blocks_[best];
+        blocks_.erase(blocks_.begin() + (long)best);
+        held_ -= r.bytes;
+        return r;
+    }
+    std::vector<Block> put(void* p, uint64_t bytes) {
+        std::lock_guard<std::mutex> lk(mu_);
+        std::vector<Block> out;
+        if (bytes > budget_) {
+            out.push_back({p, bytes});
+            return out;
+        }
+        blocks_.push_back({p, bytes});
+        held_ += bytes;
+        while (held_ > budget_) {
+            out.push_back(blocks_.front());
+            held_ -= blocks_.front().bytes;
+            blocks_.erase(blocks_.begin());
+        }
+        return out;
+    }
+    std::vector<Block> drain() {
+        std::lock_guard<std::mutex> lk(mu_);
+        std::vector<Block> out;
+        out.swap(blocks_);
+        held_ = 0;
+        return out;
+    }
+    uint64_t held() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return held_;
+    }
+
+   private:
+    std::mutex mu_;
+    const uint64_t budget_;
+    uint64_t held_ = 0;
+    std::vector<Block> blocks_;
+};
+
 }  // namespace pvhost
 
 #endif  // PV_COPY_POOL_H

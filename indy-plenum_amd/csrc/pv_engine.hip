@@ -3164,7 +3164,13 @@ int pv_init(int device) {
     return PV_OK;
 }
 
+}  // extern "C"
+namespace {
+void pinned_cache_drain();
+}
+extern "C" {
 void pv_shutdown(void) {
+    pinned_cache_drain();  // freed pv_host_alloc blocks back to the system (live ones stay the caller's)
     {
         std::lock_guard<std::mutex> lk(g_mg_mu);
         mg_destroy_comms();
@@ -3267,6 +3273,18 @@ int pv_verify_batch_device(const uint8_t* d_sm, const uint64_t* d_off, uint64_t 
 }  // extern "C"
 namespace {
 pvhost::PinnedRegistry g_pinned_alloc, g_pinned_reg;
+// freed pv_host_alloc blocks kept for reuse (copy_pool.h PinnedCache), up to PV_PINNED_CACHE_MB (4 GB)
+pvhost::PinnedCache& pinned_cache() {
+    static pvhost::PinnedCache* c = [] {
+        const char* e = getenv("PV_PINNED_CACHE_MB");
+        return new pvhost::PinnedCache((e && *e ? strtoull(e, nullptr, 10) : 4096ull) << 20);
+    }();
+    return *c;
+}
+void pinned_release(const std::vector<pvhost::PinnedCache::Block>& v) {
+    for (const auto& b : v) (void)hipHostFree(b.p);
+}
+void pinned_cache_drain() { pinned_release(pinned_cache().drain()); }
 bool pv_is_pinned(const void* p, uint64_t bytes) {
     return g_pinned_alloc.contains(p, bytes) || g_pinned_reg.contains(p, bytes);
 }
@@ -3944,16 +3962,25 @@ int pv_verify_batch_multi_gpu(const uint8_t* sm, const uint64_t* sm_off, uint64_
 int pv_host_alloc(void** p, uint64_t bytes) {
     if (!p) return fail(PV_ERR_ARG, "pv_host_alloc: null pointer");
     *p = nullptr;
-    void* q = nullptr;
-    PV_HIP(hipHostMalloc(&q, std::max<uint64_t>(bytes, 64), hipHostMallocPortable), PV_ERR_ALLOC);
-    g_pinned_alloc.add(q, std::max<uint64_t>(bytes, 64));
-    *p = q;
+    bytes = std::max<uint64_t>(bytes, 64);
+    pvhost::PinnedCache::Block b = pinned_cache().take(bytes);  // a block an earlier pv_host_free released
+    if (!b.p) {
+        b.bytes = bytes;
+        if (hipHostMalloc(&b.p, bytes, hipHostMallocPortable) != hipSuccess) {
+            (void)hipGetLastError();
+            pinned_release(pinned_cache().drain());  // the cached blocks back to the system, then once more
+            PV_HIP(hipHostMalloc(&b.p, bytes, hipHostMallocPortable), PV_ERR_ALLOC);
+        }
+    }
+    g_pinned_alloc.add(b.p, b.bytes);
+    *p = b.p;
     return PV_OK;
 }
 int pv_host_free(void* p) {
     if (!p) return PV_OK;
-    if (!g_pinned_alloc.remove(p)) return fail(PV_ERR_ARG, "pv_host_free: not a pv_host_alloc block");
-    PV_HIP(hipHostFree(p), PV_ERR_ALLOC);
+    const uint64_t bytes = g_pinned_alloc.size_of(p);
+    if (!bytes || !g_pinned_alloc.remove(p)) return fail(PV_ERR_ARG, "pv_host_free: not a pv_host_alloc block");
+    pinned_release(pinned_cache().put(p, bytes));  // kept pinned for the next allocation of a similar size
     return PV_OK;
 }
 int pv_host_register(void* p, uint64_t bytes) {

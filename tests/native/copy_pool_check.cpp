@@ -67,7 +67,24 @@ int main() {
                edge_end = r.contains(blk + sizeof blk, 0), past = r.contains(blk + 4000, 97),
                before = r.contains(blk - 1, 2), other = r.contains(blk2 + 10, 246), other_past = r.contains(blk2 + 10, 247);
     const bool removed = r.remove(blk2), gone = !r.contains(blk2, 1), twice = !r.remove(blk2);
-    printf("{\"threads_per_pool\": %u, \"pool_threads_8dev_256hw\": %u, \"pool_threads_1dev_4hw\": %u, "
+    // pinned block cache (pv_host_free keeps blocks for the next pv_host_alloc of a similar size)
+    pvhost::PinnedCache pc(1000);
+    static char m1[1], m2[1], m3[1], m4[1];
+    const bool pc_empty = pc.take(10).p == nullptr;
+    const size_t ev0 = pc.put(m1, 400).size() + pc.put(m2, 300).size();  // 700 held
+    const bool pc_small = pc.take(100).p == nullptr;        // 300 > 2 x 100: not handed out
+    const bool pc_best = pc.take(250).p == m2;              // the smallest fitting block
+    const bool pc_none = pc.take(500).p == nullptr;         // 400 < 500
+    const size_t ev1 = pc.put(m3, 500).size();              // 900 held
+    auto ev2 = pc.put(m4, 300);                             // 1200 > 1000: the oldest (m1) out
+    const bool pc_evict = ev2.size() == 1 && ev2[0].p == m1 && pc.held() == 800;
+    auto big = pc.put(m1, 5000);                            // larger than the budget: straight back
+    const bool pc_big = big.size() == 1 && big[0].p == m1 && pc.held() == 800;
+    const bool pc_drain = pc.drain().size() == 2 && pc.held() == 0 && pc.take(300).p == nullptr;
+    printf("{\"pinned_cache\": {\"empty\": %d, \"no_evict\": %d, \"small\": %d, \"best\": %d, \"none\": %d, "
+           "\"evict\": %d, \"big\": %d, \"drain\": %d}, ",
+           pc_empty, ev0 + ev1 == 0, pc_small, pc_best, pc_none, pc_evict, pc_big, pc_drain);
+    printf("\"threads_per_pool\": %u, \"pool_threads_8dev_256hw\": %u, \"pool_threads_1dev_4hw\": %u, "
            "\"concurrent_devices\": {\"w0\": [%.1f, %.1f], \"w1\": [%.1f, %.1f], \"wall_ms\": %.1f, \"task_ms\": %d, "
            "\"tasks\": %u}, \"same_pool\": {\"w0\": [%.1f, %.1f], \"w1\": [%.1f, %.1f], \"wall_ms\": %.1f}, "
            "\"registry\": {\"inner\": %d, \"whole\": %d, \"edge_end\": %d, \"past\": %d, \"before\": %d, "

@@ -3,7 +3,8 @@ library includes it): every device context has its own copy pool, so the per-dev
 pv_verify_batch_multi_gpu stage their shards concurrently (the process-wide pool
 serialised them); two callers of ONE pool take turns; the pinned-range registry that lets
 pv_verify_batch skip the staging copy for pv_host_alloc / pv_host_register memory answers interior,
-edge and foreign ranges exactly. CPU only."""
+edge and foreign ranges exactly; the cache of released pinned blocks hands them out again by size. CPU
+only."""
 import json
 import os
 import subprocess
@@ -52,3 +53,9 @@ def test_pinned_registry(report):
     assert r["inner"] and r["whole"] and r["edge_end"] and r["other"]
     assert not r["past"] and not r["before"] and not r["other_past"]
     assert r["removed"] and r["gone"] and r["twice"]
+
+
+def test_pinned_block_cache(report):
+    """pv_host_free keeps released pinned blocks (up to a budget) for the next pv_host_alloc of a
+    similar size: smallest fitting block, never one more than twice the request, oldest evicted."""
+    assert all(report["pinned_cache"].values()), report["pinned_cache"]
