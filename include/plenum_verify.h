@@ -82,9 +82,9 @@ const char* pv_last_error(void);
  * library's pinned staging buffer by per-device copy threads; inputs that lie in pinned memory the
  * library allocated or registered (pv_host_alloc / pv_host_register below) are DMA'd from where they
  * are, without that copy (the offsets too when sm_off[0] == 0). Batches whose blob is >= 8 MB are
- * verified in sub-batches of 131,072 requests whose H2D transfers (on a copy stream) overlap the
- * previous sub-batch's kernels, so a large host batch costs about its PCIe time plus one sub-batch's
- * kernels.
+ * verified in sub-batches of 262,144 requests (the first and the last half-size) whose H2D transfers
+ * (on a copy stream) overlap the previous sub-batch's kernels, so a large host batch costs about its
+ * PCIe time plus one sub-batch's kernels.
  * A call of <= 2,048 requests that takes the latency path (AUTO's range for host buffers without a
  * key-repeat hint, or PV_PATH_LATENCY) and whose records are all <= 1,840 bytes is zero-copy: the
  * requests go into fixed-stride slots of the pinned staging buffer that the kernel reads over PCIe,
@@ -125,7 +125,9 @@ int pv_shard_plan(uint64_t n, int ndev, uint64_t* bounds, uint64_t* words_per_sh
  * blocks are portable (every device of the process can DMA from them). Any range inside a block is
  * recognised per call.
  *   pv_host_alloc(p, bytes)      allocate a pinned block (*p = its address)
- *   pv_host_free(p)              free a pv_host_alloc block (PV_ERR_ARG for any other pointer)
+ *   pv_host_free(p)              release a pv_host_alloc block (PV_ERR_ARG for any other pointer);
+ *                                it stays pinned in a cache (4 GB, PV_PINNED_CACHE_MB) for the next
+ *                                pv_host_alloc of a similar size, returned to the system at pv_shutdown
  *   pv_host_register(p, bytes)   pin an existing host range in place (hipHostRegister; ~50 ms per GB,
  *                                for long-lived receive buffers)
  *   pv_host_unregister(p)        undo pv_host_register (p = the registered start)

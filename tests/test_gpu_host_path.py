@@ -8,6 +8,7 @@ pv_host_register, pv_verify_batch_multi_gpu) and of its failure paths:
   * an injected staging failure (pv_test_inject) after the first sub-batch is in flight returns an
     error, and the next call -- single-device and the multi-GPU entry -- is bit-exact;
   * pv_init_devices with a device that does not exist fails without touching the primary context;
+  * released arena blocks are handed out again by size (the pinned block cache) and verify bit-exact;
   * with >= 2 GPUs (skipped on a one-GPU box): the multi-GPU entry with empty shards, a partial last
     word and a >= 8 MB blob is bit-exact."""
 import ctypes
@@ -68,6 +69,39 @@ def test_host_forms_bit_exact(native, adv400k):
         native.check(L.pv_host_unregister(reg.ctypes.data), "pv_host_unregister")
     assert not A.is_pinned(reg)
     assert L.pv_host_free(ctypes.c_void_p(reg.ctypes.data)) != 0  # not an arena block
+
+
+def test_arena_blocks_reused_after_free(native, adv400k):
+    """pv_host_free keeps a released block pinned for the next pv_host_alloc of a similar size (at
+    most twice the request); a released block is no longer reported as the caller's pinned memory;
+    a batch built in reused blocks is verified bit-exact."""
+    import gc
+    blob, off, pks, want = adv400k
+    L = native.lib()
+
+    def alloc(nbytes):
+        p = ctypes.c_void_p()
+        native.check(L.pv_host_alloc(ctypes.byref(p), nbytes), "pv_host_alloc")
+        return p.value
+
+    a = alloc(48 << 20)
+    native.check(L.pv_host_free(ctypes.c_void_p(a)), "pv_host_free")
+    assert L.pv_host_is_pinned(ctypes.c_void_p(a), 1) == 0
+    b = alloc(40 << 20)
+    assert b == a and L.pv_host_is_pinned(ctypes.c_void_p(a), 48 << 20) == 1
+    c = alloc(8 << 20)  # 48 MB > 2 x 8 MB: a new block
+    assert c != a
+    for q in (b, c):
+        native.check(L.pv_host_free(ctypes.c_void_p(q)), "pv_host_free")
+    n = 300000
+    o = off[:n + 1]
+    first = native.HostArena.batch(blob[:int(o[-1])], o, pks[:n])
+    addrs = sorted(x.ctypes.data for x in first)
+    del first
+    gc.collect()
+    ab, ao, ak = native.HostArena.batch(blob[:int(o[-1])], o, pks[:n])
+    assert sorted(x.ctypes.data for x in (ab, ao, ak)) == addrs
+    _check(native.verify_sm_batch(ab, ao, ak), want[:n], "reused arena")
 
 
 def test_injected_stage_failure_then_exact(native, adv400k):
