@@ -2940,6 +2940,11 @@ void lane_free_buffers(Work& w, KeyWork& kw) {
 void ctx_free();
 // Builds g_ctxs[device] (caller: g_mus[device] held, DevScope(device) active, context not built yet):
 // streams and events, the fixed-base tables, the workspace. Sets the calling thread's HIP device.
+bool env_flag_devscope() {
+    const char* e = getenv("PV_EVENT_DEVSCOPE");
+    return !(e && *e == '0');
+}
+
 int ctx_init_parts(int device) {
     PV_HIP(hipSetDevice(device), PV_ERR_NO_DEVICE);
     hipDeviceProp_t prop;
@@ -2957,11 +2962,15 @@ int ctx_init_parts(int device) {
 #else
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.kstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
 #endif
-    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_keys_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
-    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    // stream-to-stream hand-overs inside the engine (one device, never read by the host) are recorded with
+    // a device-scope release instead of the default system-scope fence: headline step 2.612-2.618 against
+    // 2.620-2.624 ms interleaved (profiles/r05/ab_event_devscope.txt); PV_EVENT_DEVSCOPE=0 restores it
+    const unsigned evf = hipEventDisableTiming | (env_flag_devscope() ? hipEventReleaseToDevice : 0u);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_keys_ready, evf), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, evf), PV_ERR_NO_DEVICE);
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.fstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
-    for (auto& e : g_ctx.ev_chain) PV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), PV_ERR_NO_DEVICE);
-    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_prep_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    for (auto& e : g_ctx.ev_chain) PV_HIP(hipEventCreateWithFlags(&e, evf), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_prep_done, evf), PV_ERR_NO_DEVICE);
 #if PV_SIDE_PRIO
     {
         // Straus-side requests (one-off keys) are a short dependent chain of small grids; a
@@ -2974,13 +2983,13 @@ int ctx_init_parts(int device) {
 #else
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.sstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
 #endif
-    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_straus_done, evf), PV_ERR_NO_DEVICE);
 #if PV_COMB_B_EARLY
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.bstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
 #endif
-    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_start, hipEventDisableTiming), PV_ERR_NO_DEVICE);
-    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
-    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, hipEventDisableTiming), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_start, evf), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_done, evf), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, evf), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_verdict_copied, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     {
         // the host path's copy stream at the greatest priority: the runtime keeps such streams on hardware
