@@ -41,6 +41,12 @@ static constexpr int PV_BLOCK = 256;
 // per key (pv_key_chain_quad_kernel, round 1); 0 = one lane per key (pv_key_chain_kernel)
 #define PV_CHAIN_MODE 2
 #endif
+// an integer from the environment (A/B knobs read once at first use), or dflt
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+
 #ifndef PV_COMB_A_MINBLOCKS
 #define PV_COMB_A_MINBLOCKS 3
 #endif
@@ -2818,6 +2824,8 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
                                g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #if PV_STRAUS_WIDE_B
+            // (run beside the table kernel on the side stream it gains nothing: the table kernel's blocks hold
+            // every slot, profiles/r05/ab_straus_fork_b.txt)
             PV_LAUNCH_BC2(pv_straus_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
                                gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
@@ -3466,10 +3474,6 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
 #endif
 static constexpr uint64_t PV_PIPE_MAX = 64;                // sub-batches per call (copy events)
 static constexpr uint64_t PV_PIPE_MIN_BLOB = 8ull << 20;   // smaller blobs: one piece
-static int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e && *e ? atoi(e) : dflt;
-}
 static uint64_t pipe_sub() {
     static const uint64_t v = [] {
         const char* e = getenv("PV_PIPE_SUB");
