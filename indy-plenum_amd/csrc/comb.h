@@ -471,29 +471,12 @@ static_assert(PV_BC2_TOP_ENT <= PV_BC2_ENT, "top row larger than a full row");
 // total > P (per lane): positions total - 1 .. 0 with the stage / digit objects mapping the extra
 // positions to other niels rows -- a cached key's radix-65536 rows (pv_kc_wide: [k](-A) as 16 more
 // niels additions in the same loop).
-template <int P, class BStage, class Digit>
-PV_HD void pv_comb_b_acc_w(ge_p3& acc, const BStage& st, const Digit& digit, int total = P) {
-    int f = digit(total - 1);
-    st.stage(total - 1, f < 0 ? -f : f);
-    {
-        uint32_t w[20];
-        st.staged(0, w);
-        fe ypx, ymx, h;
-        pv_sel_pm(ypx, ymx, w, f < 0);
-        f = digit(total - 2);
-        st.stage(total - 2, f < 0 ? -f : f);
-        fe_sub(acc.X, ypx, ymx);
-        fe_carry(acc.X, acc.X);
-        fe_add(acc.Y, ypx, ymx);
-        fe_carry(acc.Y, acc.Y);
-        fe_0(acc.Z);
-        acc.Z.v[0] = 2;
-        fe_const(h, PV_INV2);
-        fe_mul(acc.T, acc.X, acc.Y);
-        fe_mul(acc.T, acc.T, h);
-    }
+// Niels additions of positions jtop .. 0 into acc; f = the digit of position jtop, whose entry is
+// already staging (st.stage(jtop, |f|)).
+template <class BStage, class Digit>
+PV_HD void pv_comb_b_steps_w(ge_p3& acc, const BStage& st, const Digit& digit, int f, int jtop) {
     ge_p1p1 t;
-    for (int j = total - 2; j >= 0; j--) {
+    for (int j = jtop; j >= 0; j--) {
         const bool neg = f < 0;
         uint32_t w[20];
         st.staged(0, w);
@@ -520,6 +503,39 @@ PV_HD void pv_comb_b_acc_w(ge_p3& acc, const BStage& st, const Digit& digit, int
         fe_sub(t.T, d, c);
         ge_niels_p1p1_to_p3(acc, t);
     }
+}
+
+template <int P, class BStage, class Digit>
+PV_HD void pv_comb_b_acc_w(ge_p3& acc, const BStage& st, const Digit& digit, int total = P) {
+    int f = digit(total - 1);
+    st.stage(total - 1, f < 0 ? -f : f);
+    {
+        uint32_t w[20];
+        st.staged(0, w);
+        fe ypx, ymx, h;
+        pv_sel_pm(ypx, ymx, w, f < 0);
+        f = digit(total - 2);
+        st.stage(total - 2, f < 0 ? -f : f);
+        fe_sub(acc.X, ypx, ymx);
+        fe_carry(acc.X, acc.X);
+        fe_add(acc.Y, ypx, ymx);
+        fe_carry(acc.Y, acc.Y);
+        fe_0(acc.Z);
+        acc.Z.v[0] = 2;
+        fe_const(h, PV_INV2);
+        fe_mul(acc.T, acc.X, acc.Y);
+        fe_mul(acc.T, acc.T, h);
+    }
+    pv_comb_b_steps_w(acc, st, digit, f, total - 2);
+}
+
+// acc += sum_j T[j][digit(j)], j = P-1 .. 0: the fixed-base part added into a point the caller already
+// holds (the Straus loop's epilogue adds [k2 S]B this way, pv_msm_kernel).
+template <int P, class BStage, class Digit>
+PV_HD void pv_comb_b_add_w(ge_p3& acc, const BStage& st, const Digit& digit) {
+    const int f = digit(P - 1);
+    st.stage(P - 1, f < 0 ? -f : f);
+    pv_comb_b_steps_w(acc, st, digit, f, P - 1);
 }
 
 // ---------------------------------------------------------------- wide per-key rows (key cache)

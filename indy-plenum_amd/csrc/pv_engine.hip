@@ -494,6 +494,31 @@ __device__ __forceinline__ void pv_glds16_row10_skip56(const uint4* g, uint4* l,
 // the LDS reads of the previous staged entry must be complete before its buffer is refilled
 __device__ __forceinline__ void pv_lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Wide fixed-base comb rows (comb.h PV_BC2_*): row j = entries 0..PV_BC2_ENT-1 of [d 2^(W j)] B,
+// 8 uint4 each, LDS-staged like DevBStage; 64-bit entry index (the table is ~10.7 GB at W = 24).
+template <uint32_t ENT>
+struct DevB2Stage {
+    const uint4* base;
+    uint4* lds;
+    uint32_t lane;
+    __device__ __forceinline__ void stage(int j, int d) const {
+        const uint4* e = base + ((uint64_t)j * ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4);
+        pv_lds_reads_done();
+        pv_glds16_row<PV_BCOMB_STRIDE / 4>(e, lds);
+    }
+    __device__ __forceinline__ void staged(int part, uint32_t w[20]) const {
+#pragma unroll
+        for (int q = 0; q < (part ? 3 : 5); q++) {
+            const uint4 v = lds[(5 * part + q) * 64 + lane];
+            const int lim = part ? 10 : 20;
+            if (4 * q < lim) w[4 * q] = v.x;
+            if (4 * q + 1 < lim) w[4 * q + 1] = v.y;
+            if (4 * q + 2 < lim) w[4 * q + 2] = v.z;
+            if (4 * q + 3 < lim) w[4 * q + 3] = v.w;
+        }
+    }
+};
+
 #if PV_STRAUS_HALF
 // The half-size msm's per-lane tables (DevATab layout, tile-major): entry j of table t of slot i staged
 // into the wave's [10][64] area (pv_straus_ar_xyz_staged)
@@ -742,10 +767,17 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(const uint8_t* __
 }
 
 // Kernel 2: Q = [S]B + [k](-A) by the regular-window Straus loop, encode, compare with R, ballot.
+// PV_MSM_FUSED_B: [k2 S]B is added inside the loop's epilogue (the wide comb's niels additions straight
+// into the loop's point, entries LDS-staged one addition ahead) instead of pv_straus_b_kernel writing it
+// to q for the epilogue to read
+#ifndef PV_MSM_FUSED_B
+#define PV_MSM_FUSED_B 1
+#endif
+template <int W>
 __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(const uint8_t* __restrict__ sm,
                                                               const uint64_t* __restrict__ off, uint64_t n,
                                                               const uint32_t* __restrict__ btab_g, Work wk,
-                                                              Gate gate) {
+                                                              const uint4* __restrict__ bcomb, Gate gate) {
     if (gate.off()) return;
     const uint32_t nc = gate.ncomb(), ntiles = (uint32_t)((n + PV_BLOCK - 1) / PV_BLOCK);
     // nothing for this block (or no Straus slot at all): leave before the LDS fill
@@ -754,6 +786,12 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
 #if PV_STRAUS_HALF && PV_MSM_STAGED
     __shared__ uint4 stg[PV_BLOCK / 64][10][64];
     uint4* stg_wave = &stg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0][0];
+#endif
+#if PV_STRAUS_HALF && PV_MSM_FUSED_B && !PV_MSM_STAGED
+    __shared__ uint4 stgb[PV_BLOCK / 64][PV_BCOMB_STRIDE / 4][64];
+    uint4* stgb_wave = &stgb[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0][0];
+#else
+    (void)bcomb;
 #endif
 #if !PV_STRAUS_WIDE_B
     __shared__ __attribute__((aligned(16))) uint32_t sbt[PV_BTAB_ENTRIES * PV_BTAB_STRIDE];
@@ -793,6 +831,12 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
                                 });
 #else
         const DevATab rt{wk.atab, (uint32_t)wk.stride, i, 9u};
+#if PV_MSM_FUSED_B
+        pv_straus_ar_xyz_addb(X, Y, Z, at, rt, dig, nw, [&](ge_p3& acc) {  // + [k2 S]B from the wide comb
+            pv_comb_b_add_w<Bc2<W>::POS>(acc, DevB2Stage<Bc2<W>::ENT>{bcomb, stgb_wave, threadIdx.x & 63u},
+                                         [&](int j) { return dig.fb(j); });
+        });
+#else
         pv_straus_ar_xyz(X, Y, Z, at, rt, dig, nw, [&](ge_p3& accB) {  // [k2 S]B (pv_straus_b_kernel)
 #pragma unroll
             for (int q = 0; q < 10; q++) {
@@ -802,6 +846,7 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
                 accB.T.v[q] = qs.ld(30 + q, i);
             }
         });
+#endif
 #endif
 #elif PV_STRAUS_WIDE_B
         pv_straus_a_xyz(X, Y, Z, at, dig, [&](ge_p3& accB) {  // [S]B, written by pv_straus_b_kernel
@@ -1869,30 +1914,6 @@ __device__ __forceinline__ void pv_comb_store_q(const Work& wk, const KeyWork& k
     }
 }
 
-// Wide fixed-base comb rows (comb.h PV_BC2_*): row j = entries 0..PV_BC2_ENT-1 of [d 2^(W j)] B,
-// 8 uint4 each, LDS-staged like DevBStage; 64-bit entry index (the table is ~10.7 GB at W = 24).
-template <uint32_t ENT>
-struct DevB2Stage {
-    const uint4* base;
-    uint4* lds;
-    uint32_t lane;
-    __device__ __forceinline__ void stage(int j, int d) const {
-        const uint4* e = base + ((uint64_t)j * ENT + (uint32_t)d) * (PV_BCOMB_STRIDE / 4);
-        pv_lds_reads_done();
-        pv_glds16_row<PV_BCOMB_STRIDE / 4>(e, lds);
-    }
-    __device__ __forceinline__ void staged(int part, uint32_t w[20]) const {
-#pragma unroll
-        for (int q = 0; q < (part ? 3 : 5); q++) {
-            const uint4 v = lds[(5 * part + q) * 64 + lane];
-            const int lim = part ? 10 : 20;
-            if (4 * q < lim) w[4 * q] = v.x;
-            if (4 * q + 1 < lim) w[4 * q + 1] = v.y;
-            if (4 * q + 2 < lim) w[4 * q + 2] = v.z;
-            if (4 * q + 3 < lim) w[4 * q + 3] = v.w;
-        }
-    }
-};
 
 // Per request on the comb path, first half: acc = [S]B from the wide fixed-base comb (PV_BC2_POS
 // positions: one entry conversion + PV_BC2_POS - 1 additions). Needs no per-key data, so it runs on
@@ -2760,11 +2781,13 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
                                g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #if PV_STRAUS_WIDE_B
+#if !PV_MSM_FUSED_B
             PV_LAUNCH_BC2(pv_straus_b_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, m, g_ctx.work, g_ctx.d_bc2, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #endif
-            hipLaunchKernelGGL(pv_msm_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m,
-                               g_ctx.d_btab, g_ctx.work, gate);
+#endif
+            PV_LAUNCH_BC2(pv_msm_kernel, dim3(sgrid), dim3(PV_BLOCK), 0, ss, d_sm, d_off + c0, m, g_ctx.d_btab,
+                          g_ctx.work, g_ctx.d_bc2, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #endif
             PV_HIP(hipEventRecord(g_ctx.ev_straus_done, ss), PV_ERR_LAUNCH);
@@ -2823,7 +2846,7 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             hipLaunchKernelGGL(pv_table_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m, d_pk + 32 * c0,
                                g_ctx.work, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-#if PV_STRAUS_WIDE_B
+#if PV_STRAUS_WIDE_B && !PV_MSM_FUSED_B
             // (run beside the table kernel on the side stream it gains nothing: the table kernel's blocks hold
             // every slot, profiles/r05/ab_straus_fork_b.txt)
             PV_LAUNCH_BC2(pv_straus_b_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, g_ctx.d_bc2,
@@ -2831,8 +2854,8 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
 #endif
             if ((rc = mark(PV_STAGE_MSM))) return rc;
-            hipLaunchKernelGGL(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
-                               g_ctx.d_btab, g_ctx.work, gate);
+            PV_LAUNCH_BC2(pv_msm_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m, g_ctx.d_btab,
+                          g_ctx.work, g_ctx.d_bc2, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         }
         if ((rc = mark(PV_STAGE_ENCODE))) return rc;

@@ -244,9 +244,11 @@ PV_HD void pv_straus_a_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const Dig& dig
 // to R exactly when Q' + [k2 S]B = [k2](SB - kA - R') is the identity, i.e. when libsodium's
 // encode(SB - kA) == R holds (see sc_halfsize). dig.ek(q) / dig.ek2(q): packed digits of |k1| / k2;
 // nw: windows (uniform across the wave on the device: the wave's maximum).
-template <class ATab, class RTab, class Dig, class AccB>
-PV_HD void pv_straus_ar_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const RTab& rtab, const Dig& dig, int nw,
-                            const AccB& load_accB) {
+// add_b(acc): acc += [k2 S mod L]B, in place (pv_msm_kernel: the wide fixed-base comb's niels additions
+// straight into the loop's point; pv_straus_ar_xyz: one cached addition of a point computed elsewhere).
+template <class ATab, class RTab, class Dig, class AddB>
+PV_HD void pv_straus_ar_xyz_addb(fe& X, fe& Y, fe& Z, const ATab& atab, const RTab& rtab, const Dig& dig, int nw,
+                                 const AddB& add_b) {
     ge_p3 acc;
     ge_p3_identity(acc);
     ge_p1p1 t;
@@ -271,14 +273,22 @@ PV_HD void pv_straus_ar_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const RTab& r
         if (win > 0) ge_p1p1_to_p2(X, Y, Z, t);
     }
     ge_p1p1_to_p3(acc, t);
-    ge_p3 accB;
-    load_accB(accB);
-    ge_cached cb;
-    ge_p3_to_cached(cb, accB);
-    ge_add_cached(t, acc, cb);
-    ge_p1p1_to_p3(acc, t);
+    add_b(acc);
     pv_add_a(t, acc, rtab, -1);
     ge_p1p1_to_p2(X, Y, Z, t);
+}
+template <class ATab, class RTab, class Dig, class AccB>
+PV_HD void pv_straus_ar_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const RTab& rtab, const Dig& dig, int nw,
+                            const AccB& load_accB) {
+    pv_straus_ar_xyz_addb(X, Y, Z, atab, rtab, dig, nw, [&](ge_p3& acc) {
+        ge_p3 accB;
+        load_accB(accB);
+        ge_cached cb;
+        ge_p3_to_cached(cb, accB);
+        ge_p1p1 t;
+        ge_add_cached(t, acc, cb);
+        ge_p1p1_to_p3(acc, t);
+    });
 }
 
 // The same loop with the table entries software-pipelined (as comb.h pv_comb_a_xyz_staged): st.stage(t,
