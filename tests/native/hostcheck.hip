@@ -492,7 +492,7 @@ void hc_lp_halfsize_stats(const uint8_t* k, uint32_t* stats) {
 
 // The half-size Straus path as the device runs it: pv_prepare_half (checks, +-A, -R', split of k,
 // k2 S mod L), the [j]PA and [j](-R') tables, [k2 S]B from pv_comb_b_acc_w<16> over the radix-65536
-// host table, pv_straus_ar_xyz, encoding compared with R. force_fallback: use (k, 1) as the split (the
+// host table, pv_straus_ar_xyz (and the fused epilogue's form), encoding compared with R. force_fallback: use (k, 1) as the split (the
 // lane fallback). extra_windows: run that many leading all-zero windows (a wave whose maximum exceeds
 // this lane's need).
 struct HostDig2 {
@@ -546,10 +546,19 @@ int hc_sign_open_straus_half16(const uint8_t* sm, uint64_t smlen, const uint8_t*
     pv_straus_ar_xyz(X, Y, Z, at, rt, dig, nw, [&](ge_p3& p) { p = accB; });
     // the LDS-staged loop the device runs (pv_straus_ar_xyz_staged) gives the same point
     pv_straus_ar_xyz_staged(X2, Y2, Z2, PvTabStage2<HostATab>{at, rt, 0, 0}, dig, nw, [&](ge_p3& p) { p = accB; });
-    uint32_t enc[8], enc2[8];
+    // the device's fused epilogue (pv_msm_kernel, PV_MSM_FUSED_B): [k2 S]B's niels additions straight
+    // into the loop's point (pv_comb_b_add_w) instead of one cached addition of accB
+    fe X3, Y3, Z3;
+    pv_straus_ar_xyz_addb(X3, Y3, Z3, at, rt, dig, nw, [&](ge_p3& acc) {
+        pv_comb_b_add_w<16>(acc, PvRowsStageB<HostBRows>{brows, 0, 0}, [&](int j) { return fb[j]; });
+    });
+    uint32_t enc[8], enc2[8], enc3[8];
     ge_p2_tobytes(enc, X, Y, Z);
     ge_p2_tobytes(enc2, X2, Y2, Z2);
-    if (!pv_words_equal(enc, enc2)) return -1;
+    ge_p2_tobytes(enc3, X3, Y3, Z3);
+    // the fused form adds in another order: the same point whenever every operand is a curve point (the
+    // addition law is complete); a request whose R or A failed its checks is rejected either way
+    if (!pv_words_equal(enc, enc2) || (ok && !pv_words_equal(enc, enc3))) return -1;
     return ok && pv_words_equal(enc, in.R);
 }
 
