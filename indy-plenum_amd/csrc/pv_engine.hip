@@ -773,6 +773,11 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(const uint8_t* __
 #ifndef PV_MSM_FUSED_B
 #define PV_MSM_FUSED_B 1
 #endif
+// PV_MSM_SORT: the msm kernel regroups each 256-slot tile's lanes by window count (below)
+#ifndef PV_MSM_SORT
+#define PV_MSM_SORT 1
+#endif
+static constexpr int PV_MSM_SORT_CLS = 8;
 template <int W>
 __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(const uint8_t* __restrict__ sm,
                                                               const uint64_t* __restrict__ off, uint64_t n,
@@ -786,6 +791,10 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
 #if PV_STRAUS_HALF && PV_MSM_STAGED
     __shared__ uint4 stg[PV_BLOCK / 64][10][64];
     uint4* stg_wave = &stg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)][0][0];
+#endif
+#if PV_STRAUS_HALF && PV_MSM_SORT
+    __shared__ uint32_t s_wcnt[PV_BLOCK / 64][PV_MSM_SORT_CLS];
+    __shared__ uint16_t s_perm[PV_BLOCK];
 #endif
 #if PV_STRAUS_HALF && PV_MSM_FUSED_B && !PV_MSM_STAGED
     __shared__ uint4 stgb[PV_BLOCK / 64][PV_BCOMB_STRIDE / 4][64];
@@ -804,8 +813,42 @@ __global__ __launch_bounds__(PV_BLOCK, PV_MSM_MINBLOCKS) void pv_msm_kernel(cons
         const uint32_t sb = gate.stile(t, ntiles);
         if ((sb + 1) * PV_BLOCK <= nc) break;
         const uint32_t i0 = sb * PV_BLOCK + threadIdx.x;  // slot
-        const bool active = i0 < n && i0 >= nc;
-        const uint32_t i = active ? i0 : (uint32_t)n - 1;  // n - 1 >= nc here: a Straus slot
+#if PV_STRAUS_HALF && PV_MSM_SORT
+        // the tile's lanes regrouped by their window count (a stable counting sort: lanes with no Straus
+        // slot first, then counts <= 30, 31, ..., >= 36), so a wave runs the largest count of lanes that
+        // need about as many: 33.1 windows per wave on average at random scalars instead of 33.9
+        // (lane mean 32.7). Block-uniform: every thread of the block takes the same tiles.
+        uint32_t src = threadIdx.x;
+        {
+            int cls = 0;
+            if (i0 < n && i0 >= nc) {
+                const int w = (int)(DevDigits{wk.digits, (uint32_t)wk.stride, i0}.nw() & 0xFFu);
+                cls = 1 + min(max(w - 30, 0), PV_MSM_SORT_CLS - 2);
+            }
+            const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+            const uint64_t below = (1ull << ln) - 1ull;
+            uint32_t rank = 0;
+            for (int c = 0; c < PV_MSM_SORT_CLS; c++) {
+                const uint64_t m = __ballot(cls == c);
+                if (c == cls) rank = (uint32_t)__popcll(m & below);
+                if (ln == 0) s_wcnt[wv][c] = (uint32_t)__popcll(m);
+            }
+            __syncthreads();
+            uint32_t base = 0;
+            for (int c = 0; c < PV_MSM_SORT_CLS; c++)
+                for (int w2 = 0; w2 < PV_BLOCK / 64; w2++)
+                    if (c < cls || (c == cls && w2 < (int)wv)) base += s_wcnt[w2][c];
+            s_perm[base + rank] = (uint16_t)threadIdx.x;
+            __syncthreads();
+            src = s_perm[threadIdx.x];
+            __syncthreads();  // the next tile rewrites s_wcnt and s_perm
+        }
+        const uint32_t is = sb * PV_BLOCK + src;
+#else
+        const uint32_t is = i0;
+#endif
+        const bool active = is < n && is >= nc;
+        const uint32_t i = active ? is : (uint32_t)n - 1;  // n - 1 >= nc here: a Straus slot
 #if !(PV_STRAUS_HALF && PV_MSM_STAGED)
         const DevATab at{wk.atab, (uint32_t)wk.stride, i};
 #endif
