@@ -714,7 +714,10 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_split_kernel(const uint8_t* __res
 
 // Kernel 1b: the cached table [j](-A), j = 0..8 (full-length path: -A from entry 1); half-size path:
 // decompression and checks of A and R, tables [j](+-A) (entries 0..8) and [j](-R') (entries 9..17).
-__global__ __launch_bounds__(PV_BLOCK, 2) void pv_table_kernel(const uint8_t* __restrict__ sm,
+#ifndef PV_TABLE_MINBLOCKS
+#define PV_TABLE_MINBLOCKS 2  // waves per SIMD (256 VGPRs; 3 spills 264 B)
+#endif
+__global__ __launch_bounds__(PV_BLOCK, PV_TABLE_MINBLOCKS) void pv_table_kernel(const uint8_t* __restrict__ sm,
                                                                 const uint64_t* __restrict__ off, uint64_t n,
                                                                 const uint8_t* __restrict__ pk, Work wk, Gate gate) {
     if (gate.off()) return;
