@@ -393,48 +393,80 @@ PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const 
 // A point whose use flag is clear (failed pre-checks, or Z = 0 on garbage input) contributes
 // z = 1 so it cannot poison the shared inverse; its encoding is then meaningless and the caller
 // masks its verdict. `src` streams the points: src.z(t, Z) and src.xy(t, X, Y) may be called more
-// than once for the same t (the device reloads instead of holding 8 points in registers), and
-// sink(t, enc, use) receives each encoding in descending t.
+// than once for the same t (the device reloads instead of holding the points in registers), and
+// sink(t, enc, use) receives each encoding once (in descending t within a group of 8). With 16 points
+// per lane the two groups of 8 share the inversion (pv_encode_batch_stream).
 #ifndef PV_ENC_BATCH_N
 #define PV_ENC_BATCH_N 8
 #endif
 static constexpr int PV_ENC_BATCH = PV_ENC_BATCH_N;
-template <class Src, class Sink>
-PV_HD void pv_encode_batch_stream(const Src& src, bool use[PV_ENC_BATCH], const Sink& sink) {
-    fe c[PV_ENC_BATCH];
+// One group of H points t0 .. t0 + H - 1 whose prefix products c[0..H-1] (of the masked z) are in c and
+// whose product's inverse is inv: the encodings, in descending t.
+template <int H, class Src, class Sink>
+PV_HD void pv_encode_group(const Src& src, const bool* use, const Sink& sink, const fe* c, fe inv, int t0) {
 #pragma unroll
-    for (int t = 0; t < PV_ENC_BATCH; t++) {
-        fe Z, z;
-        src.z(t, Z);
-        use[t] = use[t] && !fe_iszero(Z);
-        fe_1(z);
-        fe_cmov(z, Z, use[t]);
-        if (t == 0) fe_copy(c[0], z);
-        else fe_mul(c[t], c[t - 1], z);
-    }
-    fe inv;
-    fe_invert(inv, c[PV_ENC_BATCH - 1]);
-#pragma unroll
-    for (int t = PV_ENC_BATCH - 1; t >= 0; t--) {
+    for (int t = H - 1; t >= 0; t--) {
         fe zi;
         if (t > 0) {
             fe Z, z;
-            src.z(t, Z);
+            src.z(t0 + t, Z);
             fe_1(z);
-            fe_cmov(z, Z, use[t]);
+            fe_cmov(z, Z, use[t0 + t]);
             fe_mul(zi, inv, c[t - 1]);
             fe_mul(inv, inv, z);
         } else {
             fe_copy(zi, inv);
         }
         fe X, Y, x, y;
-        src.xy(t, X, Y);
+        src.xy(t0 + t, X, Y);
         fe_mul(x, X, zi);
         fe_mul(y, Y, zi);
         uint32_t enc[8];
         fe_tobytes32(enc, y);
         enc[7] ^= fe_isnegative(x) << 31;
-        sink(t, enc, use[t]);
+        sink(t0 + t, enc, use[t0 + t]);
+    }
+}
+// Prefix products c[t] = z_t0 ... z_(t0+t) of a group's masked z; sets use[] false where Z = 0.
+template <int H, class Src>
+PV_HD void pv_encode_prefix(const Src& src, bool* use, fe* c, int t0) {
+#pragma unroll
+    for (int t = 0; t < H; t++) {
+        fe Z, z;
+        src.z(t0 + t, Z);
+        use[t0 + t] = use[t0 + t] && !fe_iszero(Z);
+        fe_1(z);
+        fe_cmov(z, Z, use[t0 + t]);
+        if (t == 0) fe_copy(c[0], z);
+        else fe_mul(c[t], c[t - 1], z);
+    }
+}
+template <class Src, class Sink>
+PV_HD void pv_encode_batch_stream(const Src& src, bool use[PV_ENC_BATCH], const Sink& sink) {
+    if constexpr (PV_ENC_BATCH == 16) {
+        // two groups of 8 under ONE inversion, holding one group's prefix products at a time: group 1's
+        // product first (its prefixes are rebuilt later: 7 products), then group 0's prefixes; inv of
+        // the whole product, each group's inverse by one product with the other group's product
+        constexpr int H = 8;
+        fe c[H];
+        pv_encode_prefix<H>(src, use, c, H);
+        fe p1;
+        fe_copy(p1, c[H - 1]);
+        pv_encode_prefix<H>(src, use, c, 0);
+        fe inv, inv0, inv1;
+        fe_mul(inv, c[H - 1], p1);
+        fe_invert(inv, inv);
+        fe_mul(inv0, inv, p1);
+        fe_mul(inv1, inv, c[H - 1]);
+        pv_encode_group<H>(src, use, sink, c, inv0, 0);
+        pv_encode_prefix<H>(src, use, c, H);  // the same z (use[] already final): the same prefixes
+        pv_encode_group<H>(src, use, sink, c, inv1, H);
+    } else {
+        fe c[PV_ENC_BATCH];
+        pv_encode_prefix<PV_ENC_BATCH>(src, use, c, 0);
+        fe inv;
+        fe_invert(inv, c[PV_ENC_BATCH - 1]);
+        pv_encode_group<PV_ENC_BATCH>(src, use, sink, c, inv, 0);
     }
 }
 
