@@ -2264,17 +2264,23 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kern
         pv_comb_a_from(wk, kw, i, acc, &stg[wv][0][0]);
 }
 
-// Kernel 3: encode Q for PV_ENC_BATCH requests per lane with one shared inversion, compare with R,
-// one __ballot per request group. Wave w covers requests [64 B w, 64 B (w + 1)) (B = PV_ENC_BATCH):
-// lane l handles 64 B w + l + 64 t, t = 0..B-1, so every load is coalesced and group t's ballot is
-// verdict word B w + t. Points are re-read from q rather than held (B x 30 registers).
-static constexpr int PV_ENC_PER_WAVE = 64 * PV_ENC_BATCH;
+// Kernel 3: encode Q for B requests per lane with one shared inversion, compare with R, one __ballot
+// per request group. Wave w covers requests [64 B w, 64 B (w + 1)): lane l handles 64 B w + l + 64 t,
+// t = 0..B-1, so every load is coalesced and group t's ballot is verdict word B w + t. Points are
+// re-read from q rather than held. B = 16 (two groups of 8 under one inversion, verify_core.h) for
+// chunks of >= PV_ENC16_MIN requests, else 8: at 1M requests 1,024 waves of 16 spend 0.185-0.190 ms
+// against 0.191-0.198 for 2,048 waves of 8 (profiles/r05/ab_encode_prefetch.txt); a smaller chunk has
+// fewer waves than SIMDs either way, and its encode then lasts one wave's chain, shorter with 8.
+#ifndef PV_ENC16_MIN
+#define PV_ENC16_MIN (1u << 20)
+#endif
+template <int B>
 struct DevEncSrc {
     Soa q;
     uint32_t w, l;
     uint64_t n;
     __device__ __forceinline__ uint32_t req(int t) const {
-        const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
+        const uint32_t r = w * (64u * B) + l + 64 * t;
         return r < n ? r : 0;
     }
     __device__ __forceinline__ void z(int t, fe& o) const {
@@ -2291,6 +2297,7 @@ struct DevEncSrc {
         }
     }
 };
+template <int B>
 struct DevEncSink {
     const uint8_t* sm;
     const uint64_t* off;
@@ -2299,7 +2306,7 @@ struct DevEncSink {
     uint32_t w, l;
     uint64_t n;
     __device__ __forceinline__ void operator()(int t, const uint32_t enc[8], bool use) const {
-        const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
+        const uint32_t r = w * (64u * B) + l + 64 * t;
         const uint32_t rr0 = r < n ? r : 0;
         const uint32_t rr = slot_req ? slot_req[rr0] : rr0;
         const uint64_t raddr = reinterpret_cast<uint64_t>(sm + off[rr]);
@@ -2309,10 +2316,11 @@ struct DevEncSink {
         for (int q = 0; q < 8; q++) R[q] = mw.dw(q);
         const bool ok = use && pv_words_equal(enc, R);
         const uint64_t bits = __ballot(ok);
-        const uint32_t r0 = w * PV_ENC_PER_WAVE + 64 * t;
+        const uint32_t r0 = w * (64u * B) + 64 * t;
         if (l == 0 && r0 < n) verdict[r0 >> 6] = bits;
     }
 };
+template <int B>
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* __restrict__ sm,
                                                                  const uint64_t* __restrict__ off, uint64_t n,
                                                                  Work wk, uint64_t* __restrict__ verdict,
@@ -2321,15 +2329,15 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* _
     const bool comb = gate.keyed();  // slot order
     const uint32_t g = blockIdx.x * PV_BLOCK + threadIdx.x;
     const uint32_t w = g >> 6, l = g & 63;
-    const DevEncSrc src{Soa(wk.q, 40, wk.stride), w, l, n};
-    bool use[PV_ENC_BATCH];
+    const DevEncSrc<B> src{Soa(wk.q, 40, wk.stride), w, l, n};
+    bool use[B];
 #pragma unroll
-    for (int t = 0; t < PV_ENC_BATCH; t++) {
-        const uint32_t r = w * PV_ENC_PER_WAVE + l + 64 * t;
+    for (int t = 0; t < B; t++) {
+        const uint32_t r = w * (64u * B) + l + 64 * t;
         use[t] = r < n && wk.flags[r < n ? r : 0] != 0;
     }
-    pv_encode_batch_stream(src, use, DevEncSink{sm, off, comb ? kw.sverdict : verdict, comb ? kw.slot_req : nullptr,
-                                                w, l, n});
+    pv_encode_batch_stream_b<B>(src, use, DevEncSink<B>{sm, off, comb ? kw.sverdict : verdict,
+                                                        comb ? kw.slot_req : nullptr, w, l, n});
 }
 
 // ------------------------------------------------------------------------------------------ host
@@ -2905,9 +2913,15 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         }
         if ((rc = mark(PV_STAGE_ENCODE))) return rc;
-        const unsigned egrid = (unsigned)((m + PV_BLOCK * PV_ENC_BATCH - 1) / (PV_BLOCK * PV_ENC_BATCH));
-        hipLaunchKernelGGL(pv_encode_kernel, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+        if (m >= PV_ENC16_MIN) {
+            const unsigned egrid = (unsigned)((m + PV_BLOCK * 16 - 1) / (PV_BLOCK * 16));
+            hipLaunchKernelGGL(pv_encode_kernel<16>, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                            g_ctx.work, d_verdict + c0 / 64, kw, gate);
+        } else {
+            const unsigned egrid = (unsigned)((m + PV_BLOCK * 8 - 1) / (PV_BLOCK * 8));
+            hipLaunchKernelGGL(pv_encode_kernel<8>, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+                           g_ctx.work, d_verdict + c0 / 64, kw, gate);
+        }
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
         if (keyed) {
             hipLaunchKernelGGL(pv_unpermute_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw,

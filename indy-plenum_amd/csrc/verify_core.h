@@ -401,15 +401,24 @@ PV_HD void pv_straus(uint32_t out[8], const ATab& atab, const BTab& btab, const 
 #endif
 static constexpr int PV_ENC_BATCH = PV_ENC_BATCH_N;
 // One group of H points t0 .. t0 + H - 1 whose prefix products c[0..H-1] (of the masked z) are in c and
-// whose product's inverse is inv: the encodings, in descending t.
+// whose product's inverse is inv: the encodings, in descending t. Each point's loads are issued one
+// point ahead (the next point's z, x, y land while this one's four products run: the encode runs at one
+// or two waves per SIMD, where nothing else would cover them).
 template <int H, class Src, class Sink>
 PV_HD void pv_encode_group(const Src& src, const bool* use, const Sink& sink, const fe* c, fe inv, int t0) {
+    fe Zn, Xn, Yn;
+    src.z(t0 + H - 1, Zn);
+    src.xy(t0 + H - 1, Xn, Yn);
 #pragma unroll
     for (int t = H - 1; t >= 0; t--) {
+        const fe Z = Zn, X = Xn, Y = Yn;
+        if (t > 0) {
+            src.z(t0 + t - 1, Zn);
+            src.xy(t0 + t - 1, Xn, Yn);
+        }
         fe zi;
         if (t > 0) {
-            fe Z, z;
-            src.z(t0 + t, Z);
+            fe z;
             fe_1(z);
             fe_cmov(z, Z, use[t0 + t]);
             fe_mul(zi, inv, c[t - 1]);
@@ -417,8 +426,7 @@ PV_HD void pv_encode_group(const Src& src, const bool* use, const Sink& sink, co
         } else {
             fe_copy(zi, inv);
         }
-        fe X, Y, x, y;
-        src.xy(t0 + t, X, Y);
+        fe x, y;
         fe_mul(x, X, zi);
         fe_mul(y, Y, zi);
         uint32_t enc[8];
@@ -427,23 +435,27 @@ PV_HD void pv_encode_group(const Src& src, const bool* use, const Sink& sink, co
         sink(t0 + t, enc, use[t0 + t]);
     }
 }
-// Prefix products c[t] = z_t0 ... z_(t0+t) of a group's masked z; sets use[] false where Z = 0.
+// Prefix products c[t] = z_t0 ... z_(t0+t) of a group's masked z; sets use[] false where Z = 0. The
+// group's z are all loaded before the products.
 template <int H, class Src>
 PV_HD void pv_encode_prefix(const Src& src, bool* use, fe* c, int t0) {
+    fe Zs[H];
+#pragma unroll
+    for (int t = 0; t < H; t++) src.z(t0 + t, Zs[t]);
 #pragma unroll
     for (int t = 0; t < H; t++) {
-        fe Z, z;
-        src.z(t0 + t, Z);
-        use[t0 + t] = use[t0 + t] && !fe_iszero(Z);
+        fe z;
+        use[t0 + t] = use[t0 + t] && !fe_iszero(Zs[t]);
         fe_1(z);
-        fe_cmov(z, Z, use[t0 + t]);
+        fe_cmov(z, Zs[t], use[t0 + t]);
         if (t == 0) fe_copy(c[0], z);
         else fe_mul(c[t], c[t - 1], z);
     }
 }
-template <class Src, class Sink>
-PV_HD void pv_encode_batch_stream(const Src& src, bool use[PV_ENC_BATCH], const Sink& sink) {
-    if constexpr (PV_ENC_BATCH == 16) {
+template <int B, class Src, class Sink>
+PV_HD void pv_encode_batch_stream_b(const Src& src, bool use[B], const Sink& sink) {
+    static_assert(B == 16 || B <= 12, "pv_encode_batch_stream_b: 16, or one group of at most 12");
+    if constexpr (B == 16) {
         // two groups of 8 under ONE inversion, holding one group's prefix products at a time: group 1's
         // product first (its prefixes are rebuilt later: 7 products), then group 0's prefixes; inv of
         // the whole product, each group's inverse by one product with the other group's product
@@ -462,12 +474,16 @@ PV_HD void pv_encode_batch_stream(const Src& src, bool use[PV_ENC_BATCH], const 
         pv_encode_prefix<H>(src, use, c, H);  // the same z (use[] already final): the same prefixes
         pv_encode_group<H>(src, use, sink, c, inv1, H);
     } else {
-        fe c[PV_ENC_BATCH];
-        pv_encode_prefix<PV_ENC_BATCH>(src, use, c, 0);
+        fe c[B];
+        pv_encode_prefix<B>(src, use, c, 0);
         fe inv;
-        fe_invert(inv, c[PV_ENC_BATCH - 1]);
-        pv_encode_group<PV_ENC_BATCH>(src, use, sink, c, inv, 0);
+        fe_invert(inv, c[B - 1]);
+        pv_encode_group<B>(src, use, sink, c, inv, 0);
     }
+}
+template <class Src, class Sink>
+PV_HD void pv_encode_batch_stream(const Src& src, bool use[PV_ENC_BATCH], const Sink& sink) {
+    pv_encode_batch_stream_b<PV_ENC_BATCH>(src, use, sink);
 }
 
 // Array form (host tests).

@@ -1,0 +1,15 @@
+# round 5: encode loads issued one point ahead / a group's z all loaded first: 8 per lane (main build),
+# 16 per lane in two groups (variants/enc16p) vs the previous 8-per-lane code (variants/enc8old)
+set -o pipefail
+cd /root/repo
+export TMPDIR=/tmp
+O=gpurun_out/r05ah
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -x -q --timeout 600 --timeout-method thread > $O/parity_main.txt 2>&1 || exit $?
+PLENUM_AMD_LIB=variants/enc16p/libplenum_verify.so timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 600 --timeout-method thread > $O/parity_enc16p.txt 2>&1 || exit $?
+DS=/tmp/nym_1m.npz
+timeout -k 10 300 python3 tools/nym_workload.py --out $DS > $O/gen.txt 2>&1 || exit $?
+for r in 1 2 3; do for lib in main enc16p enc8old; do
+  if [ $lib = main ]; then L=indy-plenum_amd/plenum_amd/libplenum_verify.so; else L=variants/$lib/libplenum_verify.so; fi
+  PLENUM_AMD_LIB=$L timeout -k 10 600 python3 bench.py --dataset $DS --no-cpu-baseline --no-ingress --no-multisig --no-host-path --no-config3 --steps 20 --warmup 10 > $O/bench_$lib.$r.json 2> $O/bench_$lib.$r.log || exit $?
+done; done
