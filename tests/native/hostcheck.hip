@@ -98,6 +98,19 @@ void hc_encode_batch(uint8_t* out, const uint32_t* xyz, int* use) {
     for (int t = 0; t < PV_ENC_BATCH; t++) { memcpy(out + 32 * t, enc[t], 32); use[t] = u[t]; }
 }
 int hc_enc_batch_size(void) { return PV_ENC_BATCH; }
+// The same with 16 points in two groups of 8 under one inversion (pv_encode_batch_stream_b<16>: the
+// device's encode for chunks of >= 1M requests).
+void hc_encode_batch16(uint8_t* out, const uint32_t* xyz, int* use) {
+    fe X[16], Y[16], Z[16];
+    bool u[16];
+    for (int t = 0; t < 16; t++) {
+        memcpy(X[t].v, xyz + 30 * t, 40); memcpy(Y[t].v, xyz + 30 * t + 10, 40); memcpy(Z[t].v, xyz + 30 * t + 20, 40);
+        u[t] = use[t] != 0;
+    }
+    uint32_t enc[16][8];
+    pv_encode_batch_stream_b<16>(pv_enc_arrays{X, Y, Z}, u, pv_enc_out{enc});
+    for (int t = 0; t < 16; t++) { memcpy(out + 32 * t, enc[t], 32); use[t] = u[t]; }
+}
 
 // ---- keyed comb path on the host (comb.h): same code the comb kernels run
 struct HostBases {

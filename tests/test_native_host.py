@@ -190,10 +190,13 @@ def test_pipeline_vs_libsodium(hc, sodium, oracle):
             assert bool(hc.hc_sign_open(sm, ctypes.c_uint64(len(sm)), pk)) == sodium.sign_open_ok(sm, pk), cls
 
 
-def test_encode_batch_shared_inversion(hc):
-    """pv_encode_batch (one inversion per PV_ENC_BATCH points) == per-point x/z, y/z encoding; a
-    point with its use flag clear or Z = 0 does not disturb the others."""
-    m = hc.hc_enc_batch_size()
+@pytest.mark.parametrize("form", ["default", "two_groups_16"])
+def test_encode_batch_shared_inversion(hc, form):
+    """pv_encode_batch (one inversion per PV_ENC_BATCH points) and the 16-point two-group form
+    (pv_encode_batch_stream_b<16>) == per-point x/z, y/z encoding; a point with its use flag clear or
+    Z = 0 does not disturb the others."""
+    m = hc.hc_enc_batch_size() if form == "default" else 16
+    encode = hc.hc_encode_batch if form == "default" else hc.hc_encode_batch16
     rng = random.Random(11)
     for trial in range(200):
         pts, use, want = [], [], []
@@ -217,7 +220,7 @@ def test_encode_batch_shared_inversion(hc):
         xyz = (ctypes.c_uint32 * (30 * m))(*pts)
         u_arr = (ctypes.c_int * m)(*use)
         out = ctypes.create_string_buffer(32 * m)
-        hc.hc_encode_batch(out, xyz, u_arr)
+        encode(out, xyz, u_arr)
         for t in range(m):
             assert bool(u_arr[t]) == (want[t] is not None)
             if want[t] is not None:
