@@ -130,21 +130,15 @@ int pv_shard_plan(uint64_t n, int ndev, uint64_t* bounds, uint64_t* words_per_sh
  *                                pv_host_alloc of a similar size, returned to the system at pv_shutdown
  *   pv_host_register(p, bytes)   pin an existing host range in place (hipHostRegister; ~50 ms per GB,
  *                                for long-lived receive buffers)
- *   pv_host_unregister(p)        undo pv_host_register (p = the registered start)
+ *   pv_host_unregister(p)        undo pv_host_register (p = the registered start); a registered
+ *                                range must be unregistered before its memory is freed, or the
+ *                                library keeps treating that address range as pinned
  *   pv_host_is_pinned(p, bytes)  1 if [p, p + bytes) lies inside one such block or range */
 int pv_host_alloc(void** p, uint64_t bytes);
 int pv_host_free(void* p);
 int pv_host_register(void* p, uint64_t bytes);
 int pv_host_unregister(void* p);
 int pv_host_is_pinned(const void* p, uint64_t bytes);
-
-/* Test hook (fault injection, for the failure-path tests): PV_INJECT_STAGE makes the next `count`
- * host-buffer stagings on `device` (pv_verify_batch's copy form, a shard of pv_verify_batch_multi_gpu)
- * fail as an allocation failure would -- in the pipelined form after the first sub-batch's DMA and
- * kernels were enqueued -- so the tests can check that the call returns an error only after no copy
- * still reads the buffers, and that the next call is exact. count 0 clears it. */
-#define PV_INJECT_STAGE 1
-int pv_test_inject(int what, int device, int count);
 
 /* Device buffers in, device bitmap out. Requirements: d_sm 4-byte aligned and readable up to
  * sm_off[n] + PV_BLOB_SLACK (records themselves need no alignment), d_pk 16-byte aligned,

@@ -26,6 +26,8 @@ struct PvKeyCacheView {
     uint32_t seed;
     const uint4* wtab = nullptr;  // radix-65536 niels rows of slots < wcap (comb.h PV_KW_*), or null
     uint32_t wcap = 0;
+    uint32_t* stamp = nullptr;    // per-slot epoch of the last launch that read the slot (LRU refresh), or null
+    uint32_t epoch = 0;
 };
 
 __host__ __device__ __forceinline__ uint32_t pv_kc_hash(const uint32_t A[8], uint32_t seed) {
@@ -38,7 +40,8 @@ __host__ __device__ __forceinline__ uint32_t pv_kc_hash(const uint32_t A[8], uin
     return h;
 }
 
-// Slot of key A, or PV_KC_EMPTY. Every lane computes the same (wave-uniform) result.
+// Slot of key A, or PV_KC_EMPTY. Every lane computes the same (wave-uniform) result. A hit stamps the
+// slot with the launch's epoch (a plain vector store; every lane of a wave stores the same word).
 __device__ __forceinline__ uint32_t pv_kc_lookup(const PvKeyCacheView& kc, const uint32_t A[8]) {
     if (kc.hmask == 0) return PV_KC_EMPTY;
     uint32_t h = pv_kc_hash(A, kc.seed) & kc.hmask;
@@ -48,7 +51,10 @@ __device__ __forceinline__ uint32_t pv_kc_lookup(const PvKeyCacheView& kc, const
         uint32_t d = 0;
 #pragma unroll
         for (int q = 0; q < 8; q++) d |= kc.keys[8 * s + q] ^ A[q];
-        if (d == 0) return s;
+        if (d == 0) {
+            if (kc.stamp) kc.stamp[s] = kc.epoch;
+            return s;
+        }
         h = (h + 1) & kc.hmask;
     }
     return PV_KC_EMPTY;

@@ -28,12 +28,14 @@
 
 #include "btable.h"
 #include "copy_pool.h"
+#include "kc_admit.h"
 #include "comb.h"
 #include "keycache.h"
 #include "lp25519.h"
 #include "verify_core.h"
 #include "pv_internal.h"
 #include "../../include/plenum_verify.h"
+#include "../../include/plenum_verify_test.h"
 
 static constexpr int PV_BLOCK = 256;
 #ifndef PV_CHAIN_MODE
@@ -2362,7 +2364,6 @@ struct Ctx {
     // on its stream; a launch on a DIFFERENT stream first makes its stream wait for it, so two
     // batches enqueued on two caller streams never share the workspace at the same time.
     hipEvent_t ev_launch_done = nullptr;
-    hipEvent_t ev_verdict_copied = nullptr;  // pv_verify_batch: verdicts back (an admission may follow)
     hipStream_t last_stream = nullptr;
     uint32_t* d_btab = nullptr;
     Work work{nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
@@ -2430,15 +2431,18 @@ struct Ctx {
         std::vector<std::string> slot_key;
         std::vector<uint32_t> free_slots;
         bool broken = false;  // a failed hash-table upload left the device table stale: not consulted
-        // automatic admission (pv_key_cache_auto): a key is put on its auto_min-th appearance in
-        // pv_verify_batch calls of <= PV_KC_AUTO_MAX_BATCH requests. Appearances are counted in an
-        // open-addressing table of full keys (seen_cnt 255 = admitted), cleared when half full:
-        // the counting window is the last ~PV_KC_SEEN_H / 2 distinct keys
+        // automatic admission (pv_key_cache_auto): a key is put on its auto_min-th VERIFIED appearance
+        // in pv_verify_batch calls (every request of calls of <= PV_KC_AUTO_MAX_BATCH requests, a
+        // sample of larger ones). Appearances are counted in a SipHash-keyed table of full keys with
+        // bounded probing (kc_admit.h); an evicted key is forgotten there, so it can be re-admitted
         uint32_t auto_min = 0;
-        std::vector<uint64_t> seen_key;  // [PV_KC_SEEN_H][4]
-        std::vector<uint8_t> seen_cnt;   // [PV_KC_SEEN_H]
-        uint32_t seen_used = 0;
+        pvhost::AdmitTable seen;
         uint64_t auto_admitted = 0, auto_failed = 0;
+        // LRU refresh on use: every launch that consults the cache stamps the slots it reads with its
+        // epoch (d_stamp, pv_kc_lookup); before a put evicts, the slots stamped since the last fold
+        // move to the front of the host LRU (kc_fold_hits)
+        uint32_t* d_stamp = nullptr;
+        uint32_t epoch = 1, fold_epoch = 1;
         // pinned staging of an asynchronous put (keys, slots, hash table), reused once ev_async is done
         uint8_t* h_async = nullptr;
         uint64_t h_async_cap = 0;
@@ -2492,18 +2496,22 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 PvKeyCacheView kc_view() {
-    PvKeyCacheView v{g_ctx.kc.d_htab, g_ctx.kc.d_keys, g_ctx.kc.d_flags, g_ctx.kc.d_tab, 0u, g_ctx.kc.seed,
-                     g_ctx.kc.d_wtab, g_ctx.kc.wcap};
-    if (g_ctx.kc.enabled && !g_ctx.kc.broken && g_ctx.kc.cap > 0 && !g_ctx.kc.index.empty()) v.hmask = g_ctx.kc.hmask;
+    auto& k = g_ctx.kc;
+    PvKeyCacheView v{k.d_htab, k.d_keys, k.d_flags, k.d_tab, 0u, k.seed, k.d_wtab, k.wcap};
+    if (k.enabled && !k.broken && k.cap > 0 && !k.index.empty()) {
+        v.hmask = k.hmask;
+        v.stamp = k.d_stamp;
+        v.epoch = ++k.epoch;
+    }
     return v;
 }
 
 void kc_free() {
     auto& k = g_ctx.kc;
     for (void* p : {(void*)k.d_htab, (void*)k.d_keys, (void*)k.d_flags, (void*)k.d_tab, (void*)k.d_ntab,
-                    (void*)k.d_wtab, (void*)k.d_wscr, (void*)k.d_put_pk, (void*)k.d_put_slot})
+                    (void*)k.d_wtab, (void*)k.d_wscr, (void*)k.d_put_pk, (void*)k.d_put_slot, (void*)k.d_stamp})
         if (p) (void)hipFree(p);
-    k.d_htab = k.d_keys = k.d_flags = k.d_put_slot = k.d_wscr = nullptr;
+    k.d_htab = k.d_keys = k.d_flags = k.d_put_slot = k.d_wscr = k.d_stamp = nullptr;
     k.d_tab = k.d_ntab = k.d_wtab = nullptr;
     k.wcap = 0;
     k.d_put_pk = nullptr;
@@ -2514,8 +2522,8 @@ void kc_free() {
     k.h_async_cap = 0;
     k.cap = k.hmask = 0;
     k.broken = false;
-    k.seen_used = 0;
-    std::fill(k.seen_cnt.begin(), k.seen_cnt.end(), 0);
+    k.seen.reset();
+    k.epoch = k.fold_epoch = 1;
     k.index.clear();
     k.lru.clear();
     k.slot_key.clear();
@@ -2547,7 +2555,7 @@ int kc_upload_htab(hipStream_t s, uint32_t* hbuf = nullptr) {
     return PV_OK;
 }
 
-int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s, const uint8_t* vb = nullptr);
+int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s, const uint8_t* vb, const uint64_t* hver);
 
 int ensure_stage(uint64_t host_bytes, uint64_t dev_bytes) {
     if (host_bytes > g_ctx.h_stage_cap) {
@@ -3081,7 +3089,6 @@ int ctx_init_parts(int device) {
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_start, evf), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_b_done, evf), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_launch_done, evf), PV_ERR_NO_DEVICE);
-    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_verdict_copied, hipEventDisableTiming), PV_ERR_NO_DEVICE);
     {
         // the host path's copy stream at the greatest priority: the runtime keeps such streams on hardware
         // queues of their own instead of round-robin over GPU_MAX_HW_QUEUES (4) with the engine's streams,
@@ -3215,7 +3222,6 @@ void ctx_free() {
     if (g_ctx.ev_b_done) (void)hipEventDestroy(g_ctx.ev_b_done);
     if (g_ctx.ev_straus_done) (void)hipEventDestroy(g_ctx.ev_straus_done);
     if (g_ctx.ev_launch_done) (void)hipEventDestroy(g_ctx.ev_launch_done);
-    if (g_ctx.ev_verdict_copied) (void)hipEventDestroy(g_ctx.ev_verdict_copied);
     if (g_ctx.cstream) (void)hipStreamDestroy(g_ctx.cstream);
     if (g_ctx.ev_cstart) (void)hipEventDestroy(g_ctx.ev_cstart);
     for (hipEvent_t e : g_ctx.ev_copy) (void)hipEventDestroy(e);
@@ -3424,7 +3430,23 @@ static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* s
 #define PV_KC_AUTO_MAX_BATCH 4096  // automatic admission counts every key of host batches up to this size (a sample above)
 #endif
 static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async);
-static void kc_auto_count(const uint8_t* pk, uint64_t n, std::vector<uint8_t>& admit);
+// Automatic admission: count the VERIFIED appearances of this batch's keys (idx: the sampled requests,
+// or null for all n); the keys reaching auto_min appearances in the window are returned, at most kcap of them.
+// The verdicts are vb[i] & 1 (zero-copy verdict bytes) or bit i of hver (verdict words).
+static void kc_auto_count(const uint8_t* pk, const uint64_t* idx, uint64_t n, const uint8_t* vb, const uint64_t* hver,
+                          std::vector<uint8_t>& admit) {
+    auto& k = g_ctx.kc;
+    for (uint64_t j = 0; j < n; j++) {
+        const uint64_t i = idx ? idx[j] : j;
+        const bool ok = vb ? (vb[i] & 1u) != 0 : ((hver[i >> 6] >> (i & 63)) & 1u) != 0;
+        if (!ok) continue;  // a key is never counted on the strength of a failing signature
+        if (k.seen.count(pk + 32 * i, k.auto_min) == pvhost::AdmitTable::ADMIT) {
+            admit.insert(admit.end(), pk + 32 * i, pk + 32 * i + 32);
+            if (admit.size() >= 32ull * g_ctx.kw.kcap) break;
+        }
+    }
+}
+
 static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk, uint64_t* d_out,
                             uint64_t** dver_out, uint64_t** hver_out);
 
@@ -3531,7 +3553,7 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
                 (void)hipStreamSynchronize(s);
                 return rc;
             }
-            rc = kc_auto_after_batch(pk, n, s, vb);  // returns once the verdict bytes are written
+            rc = kc_auto_after_batch(pk, n, s, vb, nullptr);  // returns once the verdict bytes are written
             if (rc) return rc;
             memset(verdict_bits, 0, (n + 7) / 8);
             for (uint64_t i = 0; i < n; i++) verdict_bits[i >> 3] |= (uint8_t)((vb[i] & 1u) << (i & 7));
@@ -3543,7 +3565,7 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
     int rc = stage_and_launch(sm, sm_off, n, pk, nullptr, &dver, &hver);
     if (rc) return rc;
     PV_HIP(hipMemcpyAsync(hver, dver, (n + 63) / 64 * 8, hipMemcpyDeviceToHost, g_ctx.stream), PV_ERR_LAUNCH);
-    rc = kc_auto_after_batch(pk, n, g_ctx.stream);
+    rc = kc_auto_after_batch(pk, n, g_ctx.stream, nullptr, hver);
     if (rc) return rc;
     memcpy(verdict_bits, hver, (n + 7) / 8);  // little-endian words, LSB-first bits
     return PV_OK;
@@ -3830,40 +3852,36 @@ bool pv_spin_verdict_bytes(const uint8_t* vb, uint64_t n) {
 }
 
 // Automatic key-cache admission after a host-buffer batch whose verdicts are the last thing enqueued on
-// `s`: keys seen auto_min times get their tables built right behind the batch on the same stream; only
-// the verdicts are waited for, the build overlaps the caller's next steps (the next launch is ordered
-// after it). Returns once the verdicts are on the host (vb: zero-copy verdict bytes, spun on when no key
-// is admitted).
-int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s, const uint8_t* vb) {
+// `s`. Waits for the verdicts first (vb: zero-copy verdict bytes, spun on; else the verdict words hver
+// copied back on `s`), then counts the keys of the requests that VERIFIED -- a request with a failing
+// signature never counts towards its key's admission, so senders without a valid signature cannot make
+// the node build tables or evict its signers (plenum/server/client_authn.py:84-118: every signature is
+// untrusted input). The admitted keys' tables are built right behind the batch on the engine stream;
+// the call does not wait for the build (the next launch is stream-ordered after it).
+int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s, const uint8_t* vb, const uint64_t* hver) {
     auto& k = g_ctx.kc;
+    if (!(vb && pv_spin_verdict_bytes(vb, n))) PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
+    if (!(k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken)) return PV_OK;
     std::vector<uint8_t> admit;
-    if (k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken) {
-        if (n <= PV_KC_AUTO_MAX_BATCH) {
-            kc_auto_count(pk, n, admit);
-        } else {  // a large batch counts a sample: one request's key from each block of ceil(n / 4,096), at a
-                  // hashed position in the block (a fixed stride would alias with periodic signer orders)
-            const uint64_t stride = (n + PV_KC_AUTO_MAX_BATCH - 1) / PV_KC_AUTO_MAX_BATCH;
-            std::vector<uint8_t> sample;
-            sample.reserve(32 * (n / stride + 1));
-            for (uint64_t b = 0, t = 0; b < n; b += stride, t++) {
-                const uint64_t i = b + ((t * 0x9E3779B97F4A7C15ull) >> 40) % std::min(stride, n - b);
-                sample.insert(sample.end(), pk + 32 * i, pk + 32 * i + 32);
-            }
-            kc_auto_count(sample.data(), sample.size() / 32, admit);
-        }
+    if (n <= PV_KC_AUTO_MAX_BATCH) {
+        kc_auto_count(pk, nullptr, n, vb, hver, admit);
+    } else {  // a large batch counts a sample: one request from each block of ceil(n / 4,096), at a
+              // hashed position in the block (a fixed stride would alias with periodic signer orders)
+        const uint64_t stride = (n + PV_KC_AUTO_MAX_BATCH - 1) / PV_KC_AUTO_MAX_BATCH;
+        std::vector<uint64_t> sample;
+        sample.reserve(n / stride + 1);
+        for (uint64_t b = 0, t = 0; b < n; b += stride, t++)
+            sample.push_back(b + ((t * 0x9E3779B97F4A7C15ull) >> 40) % std::min(stride, n - b));
+        kc_auto_count(pk, sample.data(), sample.size(), vb, hver, admit);
     }
-    if (!admit.empty()) {
-        PV_HIP(hipEventRecord(g_ctx.ev_verdict_copied, s), PV_ERR_LAUNCH);
-        const std::string err = g_err;
-        if (kc_put_locked(admit.data(), admit.size() / 32, true) == PV_OK) {
-            k.auto_admitted += admit.size() / 32;
-        } else {
-            k.auto_failed += admit.size() / 32;  // the verdicts stand; the keys stay uncached
-            g_err = err;
-        }
-        PV_HIP(hipEventSynchronize(g_ctx.ev_verdict_copied), PV_ERR_LAUNCH);
-    } else if (!(vb && pv_spin_verdict_bytes(vb, n))) {
-        PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
+    if (admit.empty()) return PV_OK;
+    const std::string err = g_err;
+    if (kc_put_locked(admit.data(), admit.size() / 32, true) == PV_OK) {
+        k.auto_admitted += admit.size() / 32;
+    } else {
+        k.auto_failed += admit.size() / 32;  // the verdicts stand; the keys stay uncached and re-admissible
+        for (size_t j = 0; j < admit.size(); j += 32) k.seen.forget(admit.data() + j);
+        g_err = err;
     }
     return PV_OK;
 }
@@ -4086,13 +4104,17 @@ int pv_host_register(void* p, uint64_t bytes) {
     return PV_OK;
 }
 int pv_host_unregister(void* p) {
-    if (!g_pinned_reg.remove(p)) return fail(PV_ERR_ARG, "pv_host_unregister: not a registered range");
+    if (!p || g_pinned_reg.size_of(p) == 0) return fail(PV_ERR_ARG, "pv_host_unregister: not a registered range");
+    // the runtime first: if it refuses, the registry still describes what is pinned
     PV_HIP(hipHostUnregister(p), PV_ERR_ALLOC);
+    (void)g_pinned_reg.remove(p);
     return PV_OK;
 }
 int pv_host_is_pinned(const void* p, uint64_t bytes) { return pv_is_pinned(p, bytes) ? 1 : 0; }
 
 int pv_test_inject(int what, int device, int count) {
+    const char* on = getenv("PV_ENABLE_TEST_HOOKS");
+    if (!on || strcmp(on, "1") != 0) return fail(PV_ERR_ARG, "pv_test_inject: test hooks are disabled (PV_ENABLE_TEST_HOOKS=1)");
     if (what != PV_INJECT_STAGE) return fail(PV_ERR_ARG, "pv_test_inject: unknown fault");
     if (device < 0 || device >= PV_MAX_DEV || count < 0) return fail(PV_ERR_ARG, "pv_test_inject: bad device / count");
     std::lock_guard<std::mutex> lk(g_mus[device]);
@@ -4158,6 +4180,8 @@ int pv_key_cache_configure(uint32_t capacity) {
         (e = hipMalloc((void**)&k.d_keys, (uint64_t)capacity * 32)) != hipSuccess ||
         (e = hipMalloc((void**)&k.d_flags, (uint64_t)capacity * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&k.d_htab, (uint64_t)H * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&k.d_stamp, (uint64_t)capacity * 4)) != hipSuccess ||
+        (e = hipMemset(k.d_stamp, 0, (uint64_t)capacity * 4)) != hipSuccess ||
         (e = hipMalloc((void**)&k.d_put_pk, (uint64_t)g_ctx.kw.kcap * 32)) != hipSuccess ||
         (e = hipMalloc((void**)&k.d_put_slot, (uint64_t)g_ctx.kw.kcap * 4)) != hipSuccess ||
         (e = hipHostMalloc((void**)&k.h_async, (uint64_t)g_ctx.kw.kcap * 36 + (uint64_t)H * 4,
@@ -4270,6 +4294,30 @@ static int kc_build_tables(const std::vector<std::string>& fresh, const std::vec
     return PV_OK;
 }
 
+// LRU refresh on use: the slots that launches read since the last fold (d_stamp newer than
+// fold_epoch) move to the front of the LRU, least recently read first, so eviction takes the least
+// recently USED keys rather than the least recently put. Launches still running on other streams are
+// folded at the next eviction.
+static int kc_fold_hits() {
+    auto& k = g_ctx.kc;
+    if (!k.d_stamp || k.cap == 0) return PV_OK;
+    std::vector<uint32_t> st(k.cap);
+    PV_HIP(hipMemcpyAsync(st.data(), k.d_stamp, (uint64_t)k.cap * 4, hipMemcpyDeviceToHost, g_ctx.stream), PV_ERR_LAUNCH);
+    PV_HIP(hipStreamSynchronize(g_ctx.stream), PV_ERR_LAUNCH);
+    std::vector<std::pair<uint32_t, uint32_t>> used;  // (age of the stamp past the fold, slot), LRU order
+    for (auto it = k.lru.rbegin(); it != k.lru.rend(); ++it) {
+        const uint32_t age = st[*it] - k.fold_epoch;
+        if ((int32_t)age > 0) used.emplace_back(age, *it);
+    }
+    std::stable_sort(used.begin(), used.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (const auto& u : used) {
+        auto it = k.index.find(k.slot_key[u.second]);
+        if (it != k.index.end() && *it->second == u.second) k.lru.splice(k.lru.begin(), k.lru, it->second);
+    }
+    k.fold_epoch = k.epoch;
+    return PV_OK;
+}
+
 // pv_key_cache_put under g_mu. async (automatic admission): at most kcap new keys, nothing waited
 // for (pinned staging; the hash-table upload and ev_launch_done are stream-ordered after the build).
 static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async) {
@@ -4282,6 +4330,10 @@ static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async) {
     // The device hash table still holds the state before this call until kc_upload_htab below.
     std::vector<std::string> fresh;
     std::vector<uint32_t> fresh_slot, touched;
+    if (k.free_slots.size() < n && !k.lru.empty()) {
+        const int rc = kc_fold_hits();  // evictions ahead: take the launches' reads into account
+        if (rc != PV_OK) return rc;
+    }
     for (uint64_t i = 0; i < n; i++) {
         std::string key(reinterpret_cast<const char*>(pks + 32 * i), 32);
         auto it = k.index.find(key);
@@ -4297,6 +4349,7 @@ static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async) {
             slot = k.lru.back();
             k.lru.pop_back();
             k.index.erase(k.slot_key[slot]);
+            k.seen.forget(reinterpret_cast<const uint8_t*>(k.slot_key[slot].data()));  // re-admissible
             for (size_t f = 0; f < fresh.size(); f++)
                 if (fresh_slot[f] == slot) fresh_slot[f] = PV_KC_EMPTY;  // evicted before it was built
         }
@@ -4348,50 +4401,6 @@ static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async) {
     return rc;
 }
 
-static constexpr uint32_t PV_KC_SEEN_H = 1u << 16;
-
-// Automatic admission: count this batch's keys; the keys reaching auto_min appearances (and not yet
-// admitted in this window) are returned, at most kcap of them.
-static void kc_auto_count(const uint8_t* pk, uint64_t n, std::vector<uint8_t>& admit) {
-    auto& k = g_ctx.kc;
-    if (k.seen_key.empty()) {
-        k.seen_key.assign((size_t)PV_KC_SEEN_H * 4, 0);
-        k.seen_cnt.assign(PV_KC_SEEN_H, 0);
-    }
-    for (uint64_t i = 0; i < n; i++) {
-        uint64_t w[4];
-        memcpy(w, pk + 32 * i, 32);
-        if (k.seen_used >= PV_KC_SEEN_H / 2) {  // a new counting window
-            std::fill(k.seen_cnt.begin(), k.seen_cnt.end(), 0);
-            k.seen_used = 0;
-        }
-        uint32_t h = (uint32_t)(((w[0] ^ w[3]) * 0x9E3779B97F4A7C15ull) >> 48) & (PV_KC_SEEN_H - 1);
-        for (;;) {
-            uint8_t& c = k.seen_cnt[h];
-            uint64_t* e = &k.seen_key[(size_t)h * 4];
-            if (c == 0) {  // first appearance in this window
-                memcpy(e, w, 32);
-                c = 1;
-                k.seen_used++;
-                if (k.auto_min <= 1) {
-                    c = 255;
-                    admit.insert(admit.end(), pk + 32 * i, pk + 32 * i + 32);
-                }
-                break;
-            }
-            if (e[0] == w[0] && e[1] == w[1] && e[2] == w[2] && e[3] == w[3]) {
-                if (c != 255 && ++c >= k.auto_min) {
-                    c = 255;
-                    admit.insert(admit.end(), pk + 32 * i, pk + 32 * i + 32);
-                }
-                break;
-            }
-            h = (h + 1) & (PV_KC_SEEN_H - 1);
-        }
-        if (admit.size() >= 32ull * g_ctx.kw.kcap) break;
-    }
-}
-
 int pv_key_cache_put(const uint8_t* pks, uint64_t n) {
     std::lock_guard<std::mutex> lk(g_mu);
     auto& k = g_ctx.kc;
@@ -4406,8 +4415,7 @@ int pv_key_cache_auto(uint32_t min_seen) {
     if (g_ctx.device < 0) return fail(PV_ERR_NOT_INIT, "pv_key_cache_auto: call pv_init first");
     if (min_seen > 254) return fail(PV_ERR_ARG, "pv_key_cache_auto: min_seen above 254");
     g_ctx.kc.auto_min = min_seen;
-    g_ctx.kc.seen_used = 0;
-    std::fill(g_ctx.kc.seen_cnt.begin(), g_ctx.kc.seen_cnt.end(), 0);
+    g_ctx.kc.seen.reset();
     return PV_OK;
 }
 
@@ -4428,6 +4436,7 @@ int pv_key_cache_clear(void) {
     k.free_slots.clear();
     for (uint32_t i = k.cap; i-- > 0;) k.free_slots.push_back(i);
     for (auto& sk : k.slot_key) sk.clear();
+    k.seen.reset();  // every key may be admitted again
     const int rc = kc_upload_htab(g_ctx.stream);
     k.broken = rc != PV_OK;
     return rc;

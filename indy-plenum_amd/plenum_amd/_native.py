@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PLENUM_AMD_LIB", os.path.join(_HERE, "libplenum_verify.so"))
 
 PV_OK = 0
+PV_ERR_ARG = -4
 PV_BLOB_SLACK = 256
 PV_ABI_VERSION = 1
 PV_BUILD_COMB_FUSED = 1  # pv_build_flags(): [S]B and [k](-A) of the comb path in one kernel
@@ -254,7 +255,8 @@ class HostArena:
 
 
 def inject_stage_failures(device, count):
-    """Test hook: the next `count` host-buffer stagings on `device` fail (pv_test_inject)."""
+    """Test hook: the next `count` host-buffer stagings on `device` fail (pv_test_inject, declared in
+    include/plenum_verify_test.h; the library refuses it unless PV_ENABLE_TEST_HOOKS=1 is set)."""
     check(lib().pv_test_inject(PV_INJECT_STAGE, int(device), int(count)), "pv_test_inject")
 
 

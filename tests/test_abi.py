@@ -15,12 +15,16 @@ from oracle.base58_ref import b58decode as ref_b58decode, b58encode as ref_b58en
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "plenum_verify.h")
+TEST_HEADER = os.path.join(ROOT, "include", "plenum_verify_test.h")
 
 
-def header_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return set(re.findall(r"\b(pv_[a-z0-9_]+)\s*\(", text))
+def header_functions(path=None):
+    paths = [path] if path else [HEADER, TEST_HEADER]
+    out = set()
+    for p in paths:
+        text = re.sub(r"/\*.*?\*/", "", open(p).read(), flags=re.S)
+        out |= set(re.findall(r"\b(pv_[a-z0-9_]+)\s*\(", text))
+    return out
 
 
 @pytest.fixture(scope="module")
@@ -37,6 +41,25 @@ def test_library_exports_every_declared_symbol(native):
         assert hasattr(L, name), name
     assert declared == set(native.SIGNATURES), declared ^ set(native.SIGNATURES)
     assert L.pv_abi_version() == native.PV_ABI_VERSION
+
+
+def test_test_hooks_outside_the_product_header(native):
+    """The fault-injection hook is declared only in the test header, and refuses to act unless
+    PV_ENABLE_TEST_HOOKS=1 is set (a production caller must not be able to arm it)."""
+    assert "pv_test_inject" not in header_functions(HEADER)
+    assert header_functions(TEST_HEADER) == {"pv_test_inject"}
+    L = native.lib()
+    old = os.environ.pop("PV_ENABLE_TEST_HOOKS", None)
+    try:
+        assert L.pv_test_inject(native.PV_INJECT_STAGE, 0, 1) == native.PV_ERR_ARG
+        assert b"disabled" in L.pv_last_error()
+        os.environ["PV_ENABLE_TEST_HOOKS"] = "1"
+        assert L.pv_test_inject(native.PV_INJECT_STAGE, 0, 0) == native.PV_OK
+    finally:
+        if old is None:
+            os.environ.pop("PV_ENABLE_TEST_HOOKS", None)
+        else:
+            os.environ["PV_ENABLE_TEST_HOOKS"] = old
 
 
 def test_no_gpu_fails_loudly(native):

@@ -104,7 +104,8 @@ def test_arena_blocks_reused_after_free(native, adv400k):
     _check(native.verify_sm_batch(ab, ao, ak), want[:n], "reused arena")
 
 
-def test_injected_stage_failure_then_exact(native, adv400k):
+def test_injected_stage_failure_then_exact(native, adv400k, monkeypatch):
+    monkeypatch.setenv("PV_ENABLE_TEST_HOOKS", "1")
     blob, off, pks, want = adv400k
     k = 262144 + 999
     o = off[:k + 1]

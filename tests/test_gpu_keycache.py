@@ -248,9 +248,9 @@ def test_automatic_admission_large_host_batch(nat):
 
 def test_automatic_admission(nat, sodium, oracle, monkeypatch):
     """pv_key_cache_auto(2): a key is put into the cache behind the host batch in which it is seen
-    for the second time (no manual put); verdicts are libsodium's before, during and after the
-    admission (bad keys are admitted with their failing key-check flag), and a failing admission
-    leaves the verdicts unchanged and the keys uncached."""
+    VERIFIED for the second time (no manual put); verdicts are libsodium's before, during and after
+    the admission; keys that never verify (the bad keys, tampered-only appearances) are never
+    admitted; a failing admission leaves the verdicts unchanged and the keys uncached."""
     cases, keys, bad = _batch(sodium, oracle, seed=55, n=600)
     blob, off, pks = pack(cases)
     want = _want(sodium, cases)
@@ -259,24 +259,26 @@ def test_automatic_admission(nat, sodium, oracle, monkeypatch):
     kc.auto(2)
     nat.set_path(nat.PV_PATH_AUTO)
     from collections import Counter
-    mult = Counter(bytes(p) for p in pks)
-    distinct = set(mult)
-    repeated = {k for k, c in mult.items() if c >= 2}
-    assert 0 < len(repeated) < len(distinct)
+    ok = Counter(bytes(pks[i]) for i in range(len(cases)) if want[i])  # verified appearances per key
+    distinct = {bytes(p) for p in pks}
+    verified = set(ok)
+    repeated = {k for k, c in ok.items() if c >= 2}
+    assert 0 < len(repeated) < len(verified) < len(distinct)
     try:
         a0, _ = kc.auto_stats()
-        # every appearance counts: keys seen twice within this batch are admitted behind it
+        # keys verified twice within this batch are admitted behind it
         assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
         assert kc.stats()[0] == len(repeated) and all(kc.contains(k) for k in repeated)
         assert not any(kc.contains(k) for k in distinct - repeated)
-        # the next batch is verified with those tables; the keys seen once before are admitted now
+        # the next batch is verified with those tables; the keys verified once before are admitted now
         assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
         a1, f1 = kc.auto_stats()
-        assert a1 - a0 == len(distinct) and f1 == 0
-        assert kc.stats()[0] == len(distinct) and all(kc.contains(k) for k in keys)
+        assert a1 - a0 == len(verified) and f1 == 0
+        assert kc.stats()[0] == len(verified) and all(kc.contains(k) for k in keys)
+        assert not any(kc.contains(k) for k in distinct - verified)  # never verified: never admitted
         for _ in range(2):  # now verified from the cached tables
             assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
-        # a failing admission: verdicts stand, nothing new is cached
+        # a failing admission: verdicts stand, nothing new is cached, and the keys stay admissible
         kc.clear()
         kc.auto(2)  # a new counting window
         monkeypatch.setenv("PV_TEST_FAIL_KC_PUT_BATCH", "0")
@@ -284,8 +286,111 @@ def test_automatic_admission(nat, sodium, oracle, monkeypatch):
         assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
         monkeypatch.delenv("PV_TEST_FAIL_KC_PUT_BATCH")
         a2, f2 = kc.auto_stats()
-        assert a2 == a1 and f2 == len(distinct) and kc.stats()[0] == 0
+        assert a2 == a1 and f2 >= len(verified) and kc.stats()[0] == 0
         assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+        assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+        a3, _ = kc.auto_stats()  # the failed keys were forgotten, so they are admitted again
+        assert a3 - a2 == len(verified) and kc.stats()[0] == len(verified)
+    finally:
+        kc.auto(0)
+        kc.configure(0)
+
+
+def _signed(sodium, keys, counts, seed):
+    """counts[j] honest single-signature requests of ~300 bytes by keys[j] = (pk, sk)."""
+    rng = np.random.default_rng(seed)
+    cases = []
+    for (pk, sk), c in zip(keys, counts):
+        for _ in range(c):
+            m = bytes(rng.integers(0, 256, 260 + int(rng.integers(0, 80)), dtype=np.uint8))
+            cases.append((sodium.sign_detached(m, sk) + m, pk))
+    return cases
+
+
+def test_garbage_keys_admit_and_evict_nothing(nat, sodium, oracle):
+    """with 1,024 signers cached (a full cache) and automatic admission on, two
+    passes of 4,096 requests under 2,048 fresh garbage keys -- each key twice per pass, random
+    signatures -- admit no key and evict no signer (round 5 admitted all 2,048 and evicted the
+    signers: a key was counted whatever its verdict). Verdicts stay libsodium's (all rejects)."""
+    g = VectorGen(sodium, oracle, seed=61)
+    signers = [g.key(i) for i in range(1024)]
+    kc = nat.KeyCache
+    kc.configure(1024)
+    nat.set_path(nat.PV_PATH_AUTO)
+    try:
+        kc.put([pk for pk, _ in signers])
+        assert kc.stats() == (1024, 1024)
+        kc.auto(2)
+        rng = np.random.default_rng(62)
+        garbage = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(2048)]
+        a0, f0 = kc.auto_stats()
+        for p in range(2):
+            cases = []
+            for i in range(4096):
+                m = bytes(rng.integers(0, 256, 299, dtype=np.uint8))
+                cases.append((bytes(rng.integers(0, 256, 64, dtype=np.uint8)) + m, garbage[(i + p) % 2048]))
+            blob, off, pks = pack(cases)
+            want = _want(sodium, cases)
+            assert not want.any()
+            assert np.array_equal(nat.verify_sm_batch(blob, off, pks), want)
+        a1, f1 = kc.auto_stats()
+        assert (a1 - a0, f1 - f0) == (0, 0)
+        assert kc.stats() == (1024, 1024)
+        assert all(kc.contains(pk) for pk, _ in signers)
+        assert not any(kc.contains(k) for k in garbage)
+        # the signers' own requests still verify (from the cache), tampered ones still reject
+        cases = _signed(sodium, signers[:64], [4] * 64, seed=63)
+        cases[5] = (cases[5][0][:70] + bytes([cases[5][0][70] ^ 1]) + cases[5][0][71:], cases[5][1])
+        blob, off, pks = pack(cases)
+        assert np.array_equal(nat.verify_sm_batch(blob, off, pks), _want(sodium, cases))
+    finally:
+        kc.auto(0)
+        kc.configure(0)
+
+
+def test_lru_refresh_and_readmission(nat, sodium, oracle):
+    """Eviction takes the least recently USED key (launches stamp the slots they read; the stamps are
+    folded into the LRU before a put evicts), and an evicted key is re-admitted on its next two
+    verified appearances (round 5 kept it marked admitted until the counting window turned over)."""
+    g = VectorGen(sodium, oracle, seed=64)
+    keys = [g.key(i) for i in range(6)]
+    kc = nat.KeyCache
+    kc.configure(4)
+    nat.set_path(nat.PV_PATH_AUTO)
+    try:
+        kc.auto(2)
+        # k0..k3 admitted by their verified appearances (two each), k0 first
+        for j in range(4):
+            cases = _signed(sodium, [keys[j]], [2], seed=65 + j)
+            blob, off, pks = pack(cases)
+            assert nat.verify_sm_batch(blob, off, pks).all()
+            assert kc.contains(keys[j][0])
+        assert kc.stats() == (4, 4)
+        # k0 is used (read from the cache), k1 is not: admitting k4 evicts k1, not k0
+        for path in ("latency", "comb"):
+            nat.set_path(getattr(nat, "PV_PATH_" + path.upper()))
+            cases = _signed(sodium, [keys[0]], [3], seed=70)
+            blob, off, pks = pack(cases)
+            assert nat.verify_sm_batch(blob, off, pks).all()
+        nat.set_path(nat.PV_PATH_AUTO)
+        cases = _signed(sodium, [keys[4]], [2], seed=71)
+        blob, off, pks = pack(cases)
+        assert nat.verify_sm_batch(blob, off, pks).all()
+        assert kc.contains(keys[4][0]) and kc.contains(keys[0][0])
+        assert not kc.contains(keys[1][0])
+        # k1 comes back: re-admitted on its next two verified appearances
+        cases = _signed(sodium, [keys[1]], [1], seed=72)
+        blob, off, pks = pack(cases)
+        assert nat.verify_sm_batch(blob, off, pks).all()
+        assert not kc.contains(keys[1][0])
+        assert nat.verify_sm_batch(blob, off, pks).all()
+        assert kc.contains(keys[1][0])
+        # a tampered appearance does not count
+        cases = _signed(sodium, [keys[5]], [3], seed=73)
+        cases = [(c[0][:80] + bytes([c[0][80] ^ 4]) + c[0][81:], c[1]) for c in cases]
+        blob, off, pks = pack(cases)
+        assert not nat.verify_sm_batch(blob, off, pks).any()
+        assert not kc.contains(keys[5][0])
     finally:
         kc.auto(0)
         kc.configure(0)

@@ -1,0 +1,87 @@
+"""Automatic key-cache admission table (indy-plenum_amd/csrc/kc_admit.h, compiled here with g++
+exactly as the library includes it). VERDICT r5 item 1: the round-5 table hashed w0 ^ w3 with a fixed
+multiplier and probed without bound, so keys chosen to collide made every count walk the whole
+cluster on the node's Looper thread. Now the table's hash is keyed by a per-process random secret
+(NH + multiply-shift), a probe sequence stops at MAX_PROBE entries, and an evicted key can be admitted again.
+Only verified appearances reach this table (the engine filters by the verdicts first; the GPU
+side is tests/test_gpu_keycache.py). CPU only."""
+import json
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "native", "kc_admit_check.cpp")
+BIN = os.path.join(HERE, "native", "kc_admit_check")
+HDR = os.path.join(HERE, "..", "indy-plenum_amd", "csrc", "kc_admit.h")
+
+COUNTED, ADMIT, ALREADY, DROPPED = 0, 1, 2, 3
+
+
+@pytest.fixture(scope="module")
+def report():
+    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-o", BIN, SRC])
+    out = subprocess.run([BIN], check=True, capture_output=True, text=True, timeout=120).stdout
+    return json.loads(out)
+
+
+M64 = (1 << 64) - 1
+
+
+def bucket(words, a, mult, log2_h=17):
+    """NH (UMAC, Black et al. 1999) of the key's eight 32-bit words under the secret a, then
+    multiply-shift to log2_h bits: restated for the check."""
+    m = []
+    for w in words:
+        m += [w & 0xFFFFFFFF, w >> 32]
+    h = 0
+    for i in range(0, 8, 2):
+        h += ((m[i] + a[i]) & 0xFFFFFFFF) * ((m[i + 1] + a[i + 1]) & 0xFFFFFFFF)
+    return ((h & M64) * mult & M64) >> (64 - log2_h)
+
+
+def test_bucket_matches_restatement(report):
+    assert len(report["nh"]) == 2 and report["nh"][0]["a"] != report["nh"][1]["a"]
+    for t in report["nh"]:
+        mult = int(t["mult"], 16)
+        assert mult & 1
+        for *w, slot in t["keys"]:
+            assert bucket([int(x, 16) for x in w], t["a"], mult) == slot, (t, w)
+
+
+def test_old_hash_collisions_counted_in_bounded_time(report):
+    """32,000 keys that the round-5 hash put in ONE bucket (~5e8 probes over two passes there) are
+    spread by the keyed hash: about one probe per count, nothing dropped, every key admitted on its
+    second appearance, and the whole 64,000 counts take milliseconds."""
+    r = report["old_collide"]
+    assert r["old_buckets"] == 1
+    assert r["keys"] < r["window"]
+    assert r["counted"] == r["keys"] and r["admitted"] == r["keys"] and r["dropped"] == 0, r
+    assert r["probes"] <= 3 * 2 * r["keys"], r
+    assert r["ms"] < 500, r
+
+
+def test_known_secret_flood_is_capped(report):
+    """Even with the secret known (a test-only fixed key), keys forced into one slot cost at most
+    MAX_PROBE probes each: the tail of the cluster is dropped, not walked."""
+    r = report["flood"]
+    assert r["probes"] <= 3 * r["keys"] * r["max_probe"], r
+    assert r["dropped"] == 3 * (r["keys"] - r["max_probe"]), r  # the first MAX_PROBE keys keep counting
+    assert r["ms"] < 100, r
+
+
+def test_forget_allows_readmission(report):
+    assert report["forget"] == [COUNTED, ADMIT, ALREADY, 1, 0, COUNTED, ADMIT, ADMIT]
+
+
+def test_window_turnover(report):
+    w = report["window"]
+    assert w["used_full"] == w["window"]
+    assert w["first_again"] == COUNTED and w["used_after"] == 1
+
+
+def test_count_cost(report):
+    # one keyed probe per verified request: well under a microsecond (0.39 ms per 4,096-request call)
+    assert report["ns_per_count"] < 300, report["ns_per_count"]
