@@ -80,12 +80,15 @@ class DeviceBatch:
             self.L.pv_dev_free(p)
 
 
-def cpu_baseline(blob, off, pks, sample, target_s=10.0, config3=None):
-    """libsodium 1.0.18 crypto_sign_open (the reference's verifier) on the host's cores, over the
-    first `sample` requests of the same workload, repeated until about `target_s` seconds of CPU
-    work have run; the C oracle if libsodium is absent. With config3 = (blob, off, pks), also
-    libsodium's per-record verdicts over that whole batch (one pass, timed and returned): the
-    reference outputs the config-3 leg's GPU verdicts are checked against."""
+def cpu_baseline(blob, off, pks, sample, target_s=10.0, config3=None, share=16, share_s=5.0):
+    """libsodium 1.0.18 crypto_sign_open (the reference's verifier) over the first `sample` requests of
+    the same workload, repeated until about `target_s` seconds have run, on EVERY host CPU this process
+    may run on (len(sched_getaffinity), SURVEY §8d(i): the host's nproc) -- `value` and `cores`; then
+    the same on `share` threads (the per-GPU share of the node's cores, 128 / 8 on the MI355X nodes)
+    for about `share_s` seconds -- `per_gpu_share`. The C oracle on one thread if libsodium is absent.
+    With config3 = (blob, off, pks), also libsodium's per-record verdicts over that whole batch (one
+    pass on every CPU, timed and returned): the reference outputs the config-3 leg's GPU verdicts are
+    checked against."""
     from oracle.libsodium_ref import LibSodium, find_libsodium
     from oracle.oracle import Oracle, cpu_verdicts
     o = Oracle()
@@ -94,19 +97,23 @@ def cpu_baseline(blob, off, pks, sample, target_s=10.0, config3=None):
     fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                    ctypes.c_uint64, ctypes.c_int]
     path = find_libsodium()
-    threads = min(16, len(os.sched_getaffinity(0)))
+    nproc = len(os.sched_getaffinity(0))
     use_sodium = path is not None
     if not use_sodium:
         sample = min(sample, 2000)
-        threads = 1
+        nproc = share = 1
     off_s = np.ascontiguousarray(off[:sample + 1])
-    passes, acc, dt = 0, 0, 0.0
-    while dt < target_s and passes < 64:  # repeat passes until ~target_s of CPU work has run
-        t0 = time.perf_counter()
-        acc += fn((path or "").encode(), 1 if use_sodium else 0, blob.ctypes.data, off_s.ctypes.data,
-                  pks.ctypes.data, sample, threads)
-        dt += time.perf_counter() - t0
-        passes += 1
+
+    def run(threads, seconds):
+        passes, acc, dt = 0, 0, 0.0
+        while dt < seconds and passes < 1000:  # repeat passes until ~seconds of CPU work has run
+            t0 = time.perf_counter()
+            acc += fn((path or "").encode(), 1 if use_sodium else 0, blob.ctypes.data, off_s.ctypes.data,
+                      pks.ctypes.data, sample, threads)
+            dt += time.perf_counter() - t0
+            passes += 1
+        return passes, acc, dt
+
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -114,22 +121,29 @@ def cpu_baseline(blob, off, pks, sample, target_s=10.0, config3=None):
     except Exception:
         pass
     version = LibSodium(path).version if use_sodium else None
-    out = {"value": round(sample * passes / dt, 1), "unit": "verifies/s", "cores": threads,
+    impl = "libsodium %s at %s" % (version, path) if use_sodium else "C oracle restatement"
+    passes, acc, dt = run(nproc, target_s)
+    out = {"value": round(sample * passes / dt, 1), "unit": "verifies/s", "cores": nproc,
            "kind": "reference" if use_sodium else "port",
            "sample": "%d passes over %d requests of the same synthetic NYM workload, crypto_sign_open on %d "
-                     "threads (%s), %s" % (passes, sample, threads, cpu_model,
-                                           "libsodium %s at %s" % (version, path) if use_sodium
-                                           else "C oracle restatement"),
-           "accepted": int(acc), "seconds": round(dt, 3)}
+                     "threads = every CPU in this process's affinity set (%s), %s" % (passes, sample, nproc, cpu_model, impl),
+           "cpu_model": cpu_model, "accepted": int(acc), "seconds": round(dt, 3)}
+    share = min(share, nproc)
+    if share != nproc:
+        sp, sa, sdt = run(share, share_s)
+        out["per_gpu_share"] = {"value": round(sample * sp / sdt, 1), "cores": share, "accepted": int(sa),
+                                "seconds": round(sdt, 3),
+                                "note": "the same libsodium loop on %d threads: one GPU's share of an 8-GPU node's "
+                                        "128 cores" % share}
     verdicts = None
     if config3 is not None:
         t0 = time.perf_counter()
-        verdicts = cpu_verdicts(*config3, threads=threads)
+        verdicts = cpu_verdicts(*config3, threads=nproc)
         c3 = time.perf_counter() - t0
         out["config3"] = {"requests": len(verdicts), "verifies_per_s": round(len(verdicts) / c3, 1),
                           "accepted": int(verdicts.sum()), "seconds": round(c3, 3),
                           "note": "one pass of crypto_sign_open over the whole configs[2] batch on %d threads; "
-                                  "these verdicts are what the GPU's config3 verdicts are compared with" % threads}
+                                  "these verdicts are what the GPU's config3 verdicts are compared with" % nproc}
     return out, verdicts
 
 
@@ -404,25 +418,35 @@ def _config1_worker(_):
     return config1_python(_C1_WIRE)
 
 
-def config1_legs(wire, procs=16):
-    """configs[0] on one core and on `procs` forked processes (each runs the same 10k requests with
-    its own authenticators; aggregate = all requests / wall time). Runs before the GPU comes up."""
+def config1_legs(wire, share=16):
+    """configs[0] on one core, then on one forked process per CPU of this process's affinity set
+    (SURVEY §8d(i): the host's nproc) and on `share` processes (one GPU's share of the node's cores);
+    each process runs the same 10k requests with its own authenticators, aggregate = all requests /
+    wall time. Runs before the GPU comes up."""
     import multiprocessing as mp
     global _C1_WIRE
     one = config1_python(wire)
     if one is None:
         return None
-    procs = max(1, min(procs, len(os.sched_getaffinity(0))))
+    nproc = len(os.sched_getaffinity(0))
+
+    def pool(procs):
+        t0 = time.perf_counter()
+        with mp.get_context("fork").Pool(procs) as p:
+            parts = p.map(_config1_worker, range(procs))
+        dt = time.perf_counter() - t0
+        total = sum(x["requests"] for x in parts)
+        return {"processes": procs, "requests": total, "requests_per_s": round(total / dt, 1),
+                "accepted": sum(x["accepted"] for x in parts),
+                "note": "wall time incl. process start; each process authenticates the same 10k requests"}
+
     _C1_WIRE = wire
-    t0 = time.perf_counter()
-    with mp.get_context("fork").Pool(procs) as p:
-        parts = p.map(_config1_worker, range(procs))
-    dt = time.perf_counter() - t0
-    _C1_WIRE = None
-    total = sum(x["requests"] for x in parts)
-    one["processes"] = {"processes": procs, "requests": total, "requests_per_s": round(total / dt, 1),
-                        "accepted": sum(x["accepted"] for x in parts),
-                        "note": "wall time incl. process start; each process authenticates the same 10k requests"}
+    try:
+        one["processes"] = pool(max(1, nproc))
+        if min(share, nproc) != nproc:
+            one["processes_per_gpu_share"] = pool(max(1, min(share, nproc)))
+    finally:
+        _C1_WIRE = None
     return one
 
 
@@ -515,6 +539,12 @@ class Comm:
         _native.check(self.L.pv_memcpy_d2h(out.ctypes.data, self.d_all, 8 * self.world), "pv_memcpy_d2h")
         return out
 
+    def rccl_ranks(self):
+        """Every rank's (ncclCommCount, ncclCommUserRank) of its communicator, gathered."""
+        nr, rk = _native.comm_count()
+        both = self.allgather_u64((nr << 32) | rk)
+        return [int(x) >> 32 for x in both], [int(x) & 0xFFFFFFFF for x in both]
+
     def barrier(self):
         self.allgather_u64(self.rank)
 
@@ -528,6 +558,16 @@ class Comm:
         self.L.pv_comm_destroy()
         if self.rank == 0 and os.path.exists(self.path):
             os.remove(self.path)
+
+
+def rccl_summary(world, nranks_by_rank, user_rank_by_rank):
+    """The N > 1 line's `rccl` object: what RCCL itself reported on every rank (ncclCommCount /
+    ncclCommUserRank through pv_comm_count), so the line shows the all-gather ran over `world` ranks."""
+    return {"nranks": nranks_by_rank[0], "rank": user_rank_by_rank[0],
+            "nranks_max_over_ranks": max(nranks_by_rank), "nranks_min_over_ranks": min(nranks_by_rank),
+            "user_ranks": list(user_rank_by_rank),
+            "ok": bool(min(nranks_by_rank) == max(nranks_by_rank) == world and
+                       sorted(user_rank_by_rank) == list(range(world)))}
 
 
 def tamper_count(n):
@@ -639,6 +679,9 @@ def add_cpu_baseline(result, cb, c1=None):
     """Attach the libsodium CPU path timed on this box's host cores (rank 0, same run) to the line."""
     result["cpu_baseline"] = cb
     result["vs_cpu_baseline"] = round(result["value"] / cb["value"], 1) if cb.get("value") else None
+    share = cb.get("per_gpu_share", {}).get("value")
+    if share:
+        result["vs_cpu_baseline_per_gpu_share"] = round(result["value"] / share, 1)
     if c1:
         result["cpu_baseline"]["config1_python_authenticate"] = c1
     return result
@@ -718,8 +761,12 @@ def single_process_leg(blob, off, pks, want, world):
         ts.append(time.perf_counter() - t1)
         ok &= bool(np.array_equal(got, want))
     med = float(np.median(ts))
+    try:
+        clique = _native.multi_gpu_clique()
+    except Exception as ex:
+        clique = {"error": repr(ex)[:200]}
     return {"devices": list(devs), "requests": n, "verifies_per_s": round(n / med, 1), "seconds": round(med, 4),
-            "init_devices_s": round(init_s, 2), "ok": ok,
+            "init_devices_s": round(init_s, 2), "ok": ok, "rccl_clique": clique,
             "note": "pv_verify_batch_multi_gpu: host buffers, one worker thread per device (pinned staging + "
                     "H2D + verification on its own stream), one in-process ncclAllGather of the verdict words, "
                     "PCIe included; median of 3 calls"}
@@ -954,6 +1001,8 @@ def main():
     result = assemble_result(world, n, args.steps, args.warmup, elapsed, stage_ms, chunks, comb, nkeys,
                              float(blob.nbytes) / n, ok_local, ok_all, per_gpu_fixed=bool(args.per_gpu),
                              fused=_native.comb_fused() and n / chunks > FUSED_MIN_REQ)
+    if world > 1:
+        result["rccl"] = rccl_summary(world, *comm.rccl_ranks())
     if world > 1 and not args.no_host_path:
         # SURVEY.md §8e host traffic: each rank's shard from host buffers (pv_verify_batch: pinned
         # staging pipelined with the H2D DMA, kernels, verdicts back), on up to configs[4]'s 8M-request

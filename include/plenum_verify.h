@@ -111,12 +111,15 @@ int pv_last_zero_copy(void);
  *                               ncclAllGather over the clique (group call) and copied back from the first
  *                               device. No other cross-GPU traffic.
  *   pv_multi_gpu_devices        the devices in use (up to max), returns their count (0 = none).
+ *   pv_multi_gpu_comm_ranks     what RCCL itself reports for the clique: ncclCommCount of the first
+ *                               device's communicator, and ncclCommUserRank of each device's (up to max).
  *   pv_shard_plan               host-only: the shard bounds (ndev + 1 entries) and the verdict words
  *                               per shard (the all-gather's count) for n requests over ndev devices. */
 int pv_init_devices(uint32_t device_mask);
 int pv_verify_batch_multi_gpu(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,
                               uint8_t* verdict_bits);
 int pv_multi_gpu_devices(int* devices, int max_devices);
+int pv_multi_gpu_comm_ranks(int* nranks, int* ranks, int max_devices);
 int pv_shard_plan(uint64_t n, int ndev, uint64_t* bounds, uint64_t* words_per_shard);
 
 /* Library-owned pinned host memory: the host-fed path's input arena. A node that receives its
@@ -419,10 +422,13 @@ int pv_wire_plan(const char* json, const uint64_t* off, uint64_t n, const char* 
 /* Multi-GPU: one process per GPU. pv_comm_unique_id on rank 0, broadcast the 128 bytes by any
  * channel, pv_comm_init on every rank (after pv_init). pv_allgather_verdicts gathers
  * words_per_rank 64-bit verdict words from every rank into d_all (nranks * words_per_rank) with
- * one RCCL all-gather on `stream`. */
+ * one RCCL all-gather on `stream`. pv_comm_count reports what RCCL itself sees for this rank's
+ * communicator (ncclCommCount / ncclCommUserRank), so a multi-GPU run can show the ranks RCCL joined
+ * (plenum/server/node.py:1518-1527 is the batch feed these shards come from). */
 int pv_comm_unique_id(uint8_t out[128]);
 int pv_comm_init(int nranks, int rank, const uint8_t id[128]);
 int pv_allgather_verdicts(const uint64_t* d_local, uint64_t words_per_rank, uint64_t* d_all, void* stream);
+int pv_comm_count(int* nranks, int* rank);
 void pv_comm_destroy(void);
 
 /* Device memory helpers so hosts without a GPU framework can stage data (bench, smoke).

@@ -3915,6 +3915,17 @@ int pv_allgather_verdicts(const uint64_t* d_local, uint64_t words_per_rank, uint
     return PV_OK;
 }
 
+int pv_comm_count(int* nranks, int* rank) {
+    if (!g_ctx.comm) return fail(PV_ERR_NOT_INIT, "pv_comm_count: call pv_comm_init first");
+    int c = 0, r = -1;
+    ncclResult_t e = ncclCommCount(g_ctx.comm, &c);
+    if (e == ncclSuccess) e = ncclCommUserRank(g_ctx.comm, &r);
+    if (e != ncclSuccess) return fail(PV_ERR_COMM, std::string("ncclCommCount / ncclCommUserRank: ") + ncclGetErrorString(e));
+    if (nranks) *nranks = c;
+    if (rank) *rank = r;
+    return PV_OK;
+}
+
 void pv_comm_destroy(void) {
     if (g_ctx.comm) ncclCommDestroy(g_ctx.comm);
     g_ctx.comm = nullptr;
@@ -3977,6 +3988,18 @@ int pv_multi_gpu_devices(int* devices, int max_devices) {
     std::lock_guard<std::mutex> mg(g_mg_mu);
     for (int i = 0; i < (int)g_mg.devs.size() && i < max_devices && devices; i++) devices[i] = g_mg.devs[i];
     return (int)g_mg.devs.size();
+}
+
+int pv_multi_gpu_comm_ranks(int* nranks, int* ranks, int max_devices) {
+    std::lock_guard<std::mutex> mg(g_mg_mu);
+    if (g_mg.comms.empty()) return fail(PV_ERR_NOT_INIT, "pv_multi_gpu_comm_ranks: call pv_init_devices first");
+    int c = 0;
+    ncclResult_t e = ncclCommCount(g_mg.comms[0], &c);
+    for (int i = 0; e == ncclSuccess && i < (int)g_mg.comms.size() && i < max_devices && ranks; i++)
+        e = ncclCommUserRank(g_mg.comms[i], &ranks[i]);
+    if (e != ncclSuccess) return fail(PV_ERR_COMM, std::string("ncclCommCount / ncclCommUserRank: ") + ncclGetErrorString(e));
+    if (nranks) *nranks = c;
+    return PV_OK;
 }
 
 int pv_verify_batch_multi_gpu(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk,

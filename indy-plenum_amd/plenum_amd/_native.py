@@ -85,6 +85,8 @@ SIGNATURES = {
     "pv_verify_batch_multi_gpu": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                                  ctypes.c_void_p]),
     "pv_multi_gpu_devices": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "pv_multi_gpu_comm_ranks": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "pv_comm_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "pv_shard_plan": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, _c_u64p, _c_u64p]),
     "pv_host_alloc": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint64]),
     "pv_host_free": (ctypes.c_int, [ctypes.c_void_p]),
@@ -303,6 +305,24 @@ def ensure_devices(devices):
         raise NativeUnavailable("pv_init_devices failed: %s" % L.pv_last_error().decode(errors="replace"))
     _multi_devices = devices
     return devices
+
+
+def multi_gpu_clique():
+    """The in-process clique as RCCL reports it: {"devices": [...], "nranks": ncclCommCount,
+    "user_ranks": [ncclCommUserRank per device]} (pv_multi_gpu_devices / pv_multi_gpu_comm_ranks)."""
+    L = lib()
+    devs = (ctypes.c_int * 16)()
+    nd = L.pv_multi_gpu_devices(devs, 16)
+    nr, ranks = ctypes.c_int(), (ctypes.c_int * 16)()
+    check(L.pv_multi_gpu_comm_ranks(ctypes.byref(nr), ranks, 16), "pv_multi_gpu_comm_ranks")
+    return {"devices": list(devs[:nd]), "nranks": nr.value, "user_ranks": list(ranks[:nd])}
+
+
+def comm_count():
+    """(nranks, rank) of this process's rank communicator as RCCL reports them (pv_comm_count)."""
+    nr, rk = ctypes.c_int(), ctypes.c_int()
+    check(lib().pv_comm_count(ctypes.byref(nr), ctypes.byref(rk)), "pv_comm_count")
+    return nr.value, rk.value
 
 
 def verify_sm_batch_multi(blob, offsets, pks, devices=None):

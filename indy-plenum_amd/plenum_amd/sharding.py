@@ -80,6 +80,10 @@ class RcclGather:
         uid = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
         _native.check(self.L.pv_comm_init(world, rank, uid), "pv_comm_init")
 
+    def comm_count(self):
+        """(nranks, rank) as RCCL itself reports them for this communicator."""
+        return self._n.comm_count()
+
     @staticmethod
     def unique_id() -> bytes:
         from . import _native

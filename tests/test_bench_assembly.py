@@ -43,6 +43,23 @@ def test_assemble_result_multi_gpu(world):
     assert r["cpu_baseline"]["cores"] == 16 and r["cpu_baseline"]["kind"] == "reference"
     assert r["vs_cpu_baseline"] == round(r["value"] / 485000.0, 1)
     assert r["verdicts_ok"] is True
+    # what RCCL itself reported on every rank (pv_comm_count), as bench.main puts it into the line
+    r["rccl"] = bench.rccl_summary(world, [world] * world, list(range(world)))
+    assert r["rccl"] == {"nranks": world, "rank": 0, "nranks_max_over_ranks": world,
+                         "nranks_min_over_ranks": world, "user_ranks": list(range(world)), "ok": True}
+    bad = bench.rccl_summary(world, [world] * (world - 1) + [1], list(range(world)))
+    assert bad["nranks_min_over_ranks"] == 1 and bad["ok"] is False
+
+
+def test_cpu_baseline_fields():
+    """cpu_baseline carries the host's affinity-set count as `cores` and the per-GPU
+    share beside it; the line states the ratio against both."""
+    r = bench.assemble_result(1, 1 << 20, 20, 5, 20 * 2.7e-3, _stub_stages(2.7), 1, True, 1024, 299.0, True, None)
+    cb = {"value": 5.9e6, "unit": "verifies/s", "cores": 224, "kind": "reference", "sample": "stub",
+          "per_gpu_share": {"value": 4.8e5, "cores": 16}}
+    bench.add_cpu_baseline(r, cb, None)
+    assert r["vs_cpu_baseline"] == round(r["value"] / 5.9e6, 1)
+    assert r["vs_cpu_baseline_per_gpu_share"] == round(r["value"] / 4.8e5, 1)
 
 
 def test_assemble_result_single_gpu_straus():

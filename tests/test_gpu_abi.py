@@ -104,6 +104,7 @@ def test_multi_gpu_one_device_config3_bit_exact(native, oracle):
     assert native.ensure_devices([0]) == (0,)
     n_dev = native.lib().pv_multi_gpu_devices(None, 0)
     assert n_dev == 1
+    assert native.multi_gpu_clique() == {"devices": [0], "nranks": 1, "user_ranks": [0]}  # RCCL's own count
     got = native.verify_sm_batch_multi(blob2, off, pks2)
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
     # odd sizes: a partial last verdict word, fewer requests than one word

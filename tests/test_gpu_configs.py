@@ -195,6 +195,7 @@ def test_rccl_allgather_single_rank(native):
     import nym_workload
     blob, off, pks = nym_workload.generate(5000, 3000, workers=1)
     g = RcclGather(1, 0, RcclGather.unique_id())
+    assert g.comm_count() == (1, 0)  # what RCCL itself reports for the one-rank communicator
     got = verify_sharded(blob, off, pks, 0, 1, native.verify_sm_batch, g)
     assert got.all() and len(got) == 3000
 

@@ -165,6 +165,7 @@ def test_multi_gpu_two_or_more_devices(native, adv400k):
         pytest.skip("one GPU visible: the multi-device clique needs >= 2")
     blob, off, pks, want = adv400k
     devs = native.ensure_devices(range(G))
+    assert native.multi_gpu_clique() == {"devices": list(devs), "nranks": G, "user_ranks": list(range(G))}
     for n in (1, 63, 64 * G - 1, 64 * G + 65, 100001, len(want)):  # empty shards, partial words, >= 8 MB
         o = off[:n + 1]
         _check(native.verify_sm_batch_multi(blob[:int(o[-1])], o, pks[:n], devs), want[:n], ("multi", n))
