@@ -17,6 +17,13 @@ extern "C" {
 #define PV_INJECT_STAGE 1
 int pv_test_inject(int what, int device, int count);
 
+/* In-kernel clock of the dominant comb kernel, in a diagnostic build only (make EXTRA=-DPV_CLOCK_PROBE=1,
+ * tools/clock_probe.py): wave 0 of each pv_comb_ab_kernel workgroup stamps (s_memtime, s_memrealtime)
+ * at entry and exit; this copies (t0, t1, r0, r1) of up to max_blocks workgroups (block index mod
+ * 16,384, the last launch's) into out and returns how many; 0 in the product build (no stamps). Read-only:
+ * no environment switch needed. */
+int pv_test_clock_stamps(uint64_t* out, uint32_t max_blocks);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2247,6 +2247,26 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_a_kerne
 #ifndef PV_FUSED_MIN_REQ
 #define PV_FUSED_MIN_REQ 262144
 #endif
+// Diagnostic build only (PV_CLOCK_PROBE=1, tools/clock_probe.py; MI355X_MICROARCH "DVFS give-back"
+// item 6): wave 0 of every comb_ab workgroup stamps the shader clock (s_memtime) and the 100 MHz
+// constant clock (s_memrealtime) at entry and exit into a buffer of its own, which no other code reads;
+// the in-kernel clock is the median over workgroups of delta-memtime / delta-realtime x 100 MHz. The
+// product build compiles no stamp.
+#ifndef PV_CLOCK_PROBE
+#define PV_CLOCK_PROBE 0
+#endif
+#if PV_CLOCK_PROBE
+static constexpr uint32_t PV_CLOCK_SLOTS = 16384;  // workgroups stamped (block index mod this)
+__device__ uint64_t pv_clock_stamps[PV_CLOCK_SLOTS * 4];
+__device__ __forceinline__ void pv_clock_stamp(uint64_t& t, uint64_t& r) {
+    __builtin_amdgcn_sched_barrier(0);
+    t = __builtin_amdgcn_s_memtime();
+    r = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) alone
+    __builtin_amdgcn_sched_barrier(0);
+}
+#endif
+
 template <int W>
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                 const uint4* __restrict__ bcomb,
@@ -2254,6 +2274,10 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kern
     if (!gate.keyed() || gate.off()) return;
     const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
+#if PV_CLOCK_PROBE
+    uint64_t t0 = 0, r0 = 0;
+    pv_clock_stamp(t0, r0);
+#endif
     __shared__ uint4 stg[PV_BLOCK / 64][10][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
@@ -2264,6 +2288,17 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kern
         pv_comb_store_q(wk, kw, i, acc);
     else
         pv_comb_a_from(wk, kw, i, acc, &stg[wv][0][0]);
+#if PV_CLOCK_PROBE
+    uint64_t t1 = 0, r1 = 0;
+    pv_clock_stamp(t1, r1);
+    if (threadIdx.x == 0) {
+        uint64_t* o = pv_clock_stamps + 4ull * (blockIdx.x % PV_CLOCK_SLOTS);
+        o[0] = t0;
+        o[1] = t1;
+        o[2] = r0;
+        o[3] = r1;
+    }
+#endif
 }
 
 // Kernel 3: encode Q for B requests per lane with one shared inversion, compare with R, one __ballot
@@ -2351,7 +2386,8 @@ struct Ctx {
     int cus = 0;
     hipStream_t stream = nullptr;
     hipStream_t kstream = nullptr;           // per-key pipeline (chain + table fill), overlapped
-    hipEvent_t ev_keys_ready = nullptr;      // dedup done (main -> kstream)
+    hipEvent_t ev_keys_ready = nullptr;      // dedup done (main -> Straus side stream)
+    hipEvent_t ev_scan_done = nullptr;       // comb keys chosen (main -> kstream, before the scatter)
     hipEvent_t ev_tables_ready = nullptr;    // comb tables done (fstream -> main)
     hipStream_t fstream = nullptr;           // table fill, one launch per chain part
     hipEvent_t ev_chain[PV_CHAIN_PARTS] = {};  // chain part done (kstream -> fstream)
@@ -2645,6 +2681,12 @@ int launch_chunks(const uint8_t* d_sm, const uint64_t* d_off, uint64_t n, const 
     return rc;
 }
 
+// kstream (key chain + fill) forks from the main stream right after the scan kernel instead of after
+// the scatter (A/B switch; the chain is on the step's critical path, profiles/r06/).
+#ifndef PV_FORK_AFTER_SCAN
+#define PV_FORK_AFTER_SCAN 1
+#endif
+
 // Chunk c of the batch on `stream` (the workspace is the context's; key / fill / side streams join it).
 int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, const uint8_t* d_pk,
                  uint64_t* d_verdict, hipStream_t stream, bool latency, bool dev_choice, int evb) {
@@ -2771,12 +2813,19 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             // key-sorted slot order: comb keys' requests first, then the Straus requests
             hipLaunchKernelGGL(pv_key_scan_kernel, dim3(1), dim3(PV_SCAN_THREADS), 0, stream, kw, kc_flags);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
+            // the per-key chain (few, long-latency lanes) and the table fill run on kstream, overlapped
+            // with the scatter and the per-request prep on the main stream: the chain needs only the
+            // scan's comb-key list (comb_key, comb_cslot), so kstream forks before the scatter
+#if PV_FORK_AFTER_SCAN
+            PV_HIP(hipEventRecord(g_ctx.ev_scan_done, stream), PV_ERR_LAUNCH);
+            PV_HIP(hipStreamWaitEvent(g_ctx.kstream, g_ctx.ev_scan_done, 0), PV_ERR_LAUNCH);
+#endif
             hipLaunchKernelGGL(pv_key_scatter_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, kw);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
-            // the per-key chain (few, long-latency lanes) and the table fill run on kstream,
-            // overlapped with the per-request prep on the main stream
             PV_HIP(hipEventRecord(g_ctx.ev_keys_ready, stream), PV_ERR_LAUNCH);
+#if !PV_FORK_AFTER_SCAN
             PV_HIP(hipStreamWaitEvent(g_ctx.kstream, g_ctx.ev_keys_ready, 0), PV_ERR_LAUNCH);
+#endif
             // a chunk above PV_SPARSE_CHUNK never fills sparsely: chain and fill back to back on kstream
             // and the tables-ready event right after the fill (no event hop to fstream, no gated
             // sparse-fill launch in the dependency chain of the comb kernel)
@@ -3066,6 +3115,7 @@ int ctx_init_parts(int device) {
     // 2.620-2.624 ms interleaved (profiles/r05/ab_event_devscope.txt); PV_EVENT_DEVSCOPE=0 restores it
     const unsigned evf = hipEventDisableTiming | (env_flag_devscope() ? hipEventReleaseToDevice : 0u);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_keys_ready, evf), PV_ERR_NO_DEVICE);
+    PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_scan_done, evf), PV_ERR_NO_DEVICE);
     PV_HIP(hipEventCreateWithFlags(&g_ctx.ev_tables_ready, evf), PV_ERR_NO_DEVICE);
     PV_HIP(hipStreamCreateWithFlags(&g_ctx.fstream, hipStreamNonBlocking), PV_ERR_NO_DEVICE);
     for (auto& e : g_ctx.ev_chain) PV_HIP(hipEventCreateWithFlags(&e, evf), PV_ERR_NO_DEVICE);
@@ -3211,6 +3261,7 @@ void ctx_free() {
     if (g_ctx.stream) (void)hipStreamDestroy(g_ctx.stream);
     if (g_ctx.kstream) (void)hipStreamDestroy(g_ctx.kstream);
     if (g_ctx.ev_keys_ready) (void)hipEventDestroy(g_ctx.ev_keys_ready);
+    if (g_ctx.ev_scan_done) (void)hipEventDestroy(g_ctx.ev_scan_done);
     if (g_ctx.ev_tables_ready) (void)hipEventDestroy(g_ctx.ev_tables_ready);
     if (g_ctx.fstream) (void)hipStreamDestroy(g_ctx.fstream);
     for (hipEvent_t e : g_ctx.ev_chain)
@@ -4134,6 +4185,20 @@ int pv_host_unregister(void* p) {
     return PV_OK;
 }
 int pv_host_is_pinned(const void* p, uint64_t bytes) { return pv_is_pinned(p, bytes) ? 1 : 0; }
+
+int pv_test_clock_stamps(uint64_t* out, uint32_t max_blocks) {
+#if PV_CLOCK_PROBE
+    const uint32_t k = std::min<uint32_t>(max_blocks, PV_CLOCK_SLOTS);
+    if (!out || k == 0) return (int)PV_CLOCK_SLOTS;
+    PV_HIP(hipDeviceSynchronize(), PV_ERR_LAUNCH);
+    PV_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(pv_clock_stamps), (size_t)k * 32, 0, hipMemcpyDeviceToHost), PV_ERR_LAUNCH);
+    return (int)k;
+#else
+    (void)out;
+    (void)max_blocks;
+    return 0;
+#endif
+}
 
 int pv_test_inject(int what, int device, int count) {
     const char* on = getenv("PV_ENABLE_TEST_HOOKS");

@@ -94,6 +94,7 @@ SIGNATURES = {
     "pv_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_host_is_pinned": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "pv_test_inject": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "pv_test_clock_stamps": (ctypes.c_int, [_c_u64p, ctypes.c_uint32]),
     "pv_stream_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "pv_stream_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "pv_stream_sync": (ctypes.c_int, [ctypes.c_void_p]),

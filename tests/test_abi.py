@@ -43,11 +43,17 @@ def test_library_exports_every_declared_symbol(native):
     assert L.pv_abi_version() == native.PV_ABI_VERSION
 
 
+def L_stamps_absent(native):
+    """The product build compiles no clock stamps (PV_CLOCK_PROBE is a diagnostic build only)."""
+    return native.lib().pv_test_clock_stamps(None, 0) == 0
+
+
 def test_test_hooks_outside_the_product_header(native):
     """The fault-injection hook is declared only in the test header, and refuses to act unless
     PV_ENABLE_TEST_HOOKS=1 is set (a production caller must not be able to arm it)."""
     assert "pv_test_inject" not in header_functions(HEADER)
-    assert header_functions(TEST_HEADER) == {"pv_test_inject"}
+    assert header_functions(TEST_HEADER) == {"pv_test_inject", "pv_test_clock_stamps"}
+    assert L_stamps_absent(native)
     L = native.lib()
     old = os.environ.pop("PV_ENABLE_TEST_HOOKS", None)
     try:
