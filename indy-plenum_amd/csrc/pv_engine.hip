@@ -447,6 +447,10 @@ struct KeyWork {
     const uint4* kc_ntab;  // the same divided by Z [cap][32][129][10] (comb.h pv_comb_row_to_affine), or null
     const uint4* kc_wtab;  // radix-65536 rows of slots < kc_wcap [kc_wcap][16][32897][8] (comb.h PV_KW_*), or null
     uint32_t kc_wcap;
+    // a later sub-batch of a pipelined host call with a non-empty node cache: the keys the node cache
+    // misses are looked up in the call's shared store too; a hit there is slot | PV_CSLOT_XT
+    const uint32_t* xt_flags;
+    const uint4* xt_tab;
     uint32_t hmask;
     uint32_t kcap;
     uint32_t seed;
@@ -458,6 +462,7 @@ struct KeyWork {
     uint32_t dense_only;  // never fill sparsely (the tables outlive the chunk: pv_xtab_publish_kernel)
 };
 static constexpr uint32_t PV_EMPTY = 0xFFFFFFFFu;
+static constexpr uint32_t PV_CSLOT_XT = 0x40000000u;  // cache slot in the call's shared store (KeyWork::xt_*)
 #ifndef PV_COMB_MIN_REQ
 #define PV_COMB_MIN_REQ 48
 #endif
@@ -1123,15 +1128,22 @@ __global__ __launch_bounds__(PV_BLOCK) void pv_key_assign_kernel(uint64_t n, Key
 }
 
 // Dedup 2b (only when the node-side key cache holds keys): every distinct key id looks its key up
-// in the cache (keycache.h); key_cslot[id] = its cache slot or PV_EMPTY.
+// in the cache (keycache.h); key_cslot[id] = its cache slot or PV_EMPTY. xt (hmask != 0 only for a
+// later sub-batch of a pipelined host call): a key the cache misses is looked up in the call's shared
+// table store next, a hit there giving its slot | PV_CSLOT_XT.
 __global__ __launch_bounds__(PV_BLOCK) void pv_key_cache_probe_kernel(const uint8_t* __restrict__ pk, KeyWork kw,
-                                                                       PvKeyCacheView kc) {
+                                                                       PvKeyCacheView kc, PvKeyCacheView xt) {
     const uint32_t id = blockIdx.x * PV_BLOCK + threadIdx.x;  // grid: PV_NSEG * seg_cap ids
     const uint32_t seg = id / kw.seg_cap;
     if (seg >= PV_NSEG || id - seg * kw.seg_cap >= kw.nkeys[PV_SEG_BASE + seg * PV_SEG_STRIDE]) return;
     uint32_t A[8];
     pv_load_pk(A, pk, kw.key_owner[id]);
-    kw.key_cslot[id] = pv_kc_lookup(kc, A);
+    uint32_t s = pv_kc_lookup(kc, A);
+    if (s == PV_KC_EMPTY && xt.hmask) {
+        const uint32_t x = pv_kc_lookup(xt, A);
+        if (x != PV_KC_EMPTY) s = x | PV_CSLOT_XT;
+    }
+    kw.key_cslot[id] = s;
 }
 
 // Tables shared by the sub-batches of one pipelined host call (stage_and_launch): sub-batch 0 builds
@@ -1278,7 +1290,8 @@ __global__ __launch_bounds__(1024) void pv_key_scan_kernel(KeyWork kw, const uin
             kw.comb_key[j] = id;
             kw.comb_cslot[j] = cslot;
             // a cached key's libsodium checks ran when its table was built (the chain skips it)
-            if (cslot != PV_EMPTY) kw.key_flag[j] = kc_flags[cslot];
+            if (cslot != PV_EMPTY)
+                kw.key_flag[j] = (cslot & PV_CSLOT_XT) ? kw.xt_flags[cslot & ~PV_CSLOT_XT] : kc_flags[cslot];
             kw.key_cursor[id] = cc;
             cc += c;
         } else {
@@ -2156,14 +2169,16 @@ __device__ __forceinline__ void pv_comb_a_from(const Work& wk, const KeyWork& kw
                                                uint4* stg_wave) {
     const uint32_t id = kw.skey[i];  // comb index
     const uint32_t cslot = kw.comb_cslot[id];
-    const uint4* ktab = cslot != PV_EMPTY ? kw.kc_tab + (uint64_t)cslot * PV_COMB_POS * PV_COMB_ENT * 10
-                                          : kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10;
+    const bool xt = cslot != PV_EMPTY && (cslot & PV_CSLOT_XT);
+    const uint4* ktab = cslot == PV_EMPTY ? kw.ctab + (uint64_t)id * PV_COMB_POS * PV_COMB_ENT * 10
+                        : xt ? kw.xt_tab + (uint64_t)(cslot & ~PV_CSLOT_XT) * PV_COMB_POS * PV_COMB_ENT * 10
+                             : kw.kc_tab + (uint64_t)cslot * PV_COMB_POS * PV_COMB_ENT * 10;
     const Soa qs(wk.q, 40, wk.stride);
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     fe X, Y, Z;
 #if PV_COMB_PIPELINE
     // a cached key with affine rows: additions without the Z1 Z2 product (comb.h pv_comb_row_to_affine)
-    const bool aff = cslot != PV_EMPTY && kw.kc_ntab;
+    const bool aff = cslot != PV_EMPTY && !xt && kw.kc_ntab;
     if (aff) ktab = kw.kc_ntab + (uint64_t)cslot * PV_COMB_POS * PV_COMB_ENT * 10;
     pv_comb_a_xyz_staged(X, Y, Z, acc, DevCombStage{ktab, stg_wave, threadIdx.x & 63u, aff}, dig);
 #else
@@ -2723,12 +2738,22 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
         // batch can be that small) skip dedup and go Straus. A key in the node-side key cache has
         // its comb table already built: its requests take the comb path at any count.
         PvKeyCacheView kcv = kc_view();
+        PvKeyCacheView xtv{nullptr, nullptr, nullptr, nullptr, 0u, 0u};
         const uint32_t* kc_flags = g_ctx.kc.d_flags;
         const uint4* kc_tab = g_ctx.kc.d_tab;
+        const bool node_kc = kcv.hmask != 0;
+        bool xt_only = false;
         if (g_ctx.xt_use) {  // a later sub-batch of a pipelined host call: the call's shared tables
-            kcv = PvKeyCacheView{g_ctx.xt.htab, g_ctx.xt.keys, g_ctx.xt.flags, g_ctx.xt.tab, PV_XT_HASH - 1, g_ctx.kw.seed};
-            kc_flags = g_ctx.xt.flags;
-            kc_tab = g_ctx.xt.tab;
+            const PvKeyCacheView xv{g_ctx.xt.htab, g_ctx.xt.keys, g_ctx.xt.flags, g_ctx.xt.tab, PV_XT_HASH - 1,
+                                    g_ctx.kw.seed};
+            if (node_kc) {  // the node cache first, then the shared store for the keys it misses
+                xtv = xv;
+            } else {        // the shared store is the only view
+                kcv = xv;
+                kc_flags = g_ctx.xt.flags;
+                kc_tab = g_ctx.xt.tab;
+                xt_only = true;
+            }
         }
         const bool kc_active = kcv.hmask != 0;
         const bool keyed = g_ctx.path == PV_PATH_COMB ||
@@ -2745,9 +2770,11 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
         kw.seg_cap = (uint32_t)((((m + 63) / 64) + PV_NSEG - 1) / PV_NSEG * 64);
         kw.lat_choice = dev_choice ? 1u : 0u;
         kw.kc_tab = kc_tab;
-        kw.kc_ntab = g_ctx.xt_use ? nullptr : g_ctx.kc.d_ntab;
-        kw.kc_wtab = g_ctx.xt_use ? nullptr : g_ctx.kc.d_wtab;
-        kw.kc_wcap = g_ctx.xt_use ? 0u : g_ctx.kc.wcap;
+        kw.kc_ntab = xt_only ? nullptr : g_ctx.kc.d_ntab;
+        kw.kc_wtab = xt_only ? nullptr : g_ctx.kc.d_wtab;
+        kw.kc_wcap = xt_only ? 0u : g_ctx.kc.wcap;
+        kw.xt_flags = xtv.hmask ? g_ctx.xt.flags : nullptr;
+        kw.xt_tab = xtv.hmask ? g_ctx.xt.tab : nullptr;
         kw.dense_only = 0;
         if (g_ctx.xt_fill) {  // sub-batch 0 of a pipelined host call: its tables go to the shared store, whole
             kw.ctab = g_ctx.xt.tab;
@@ -2806,7 +2833,7 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             if (kc_active) {
                 hipLaunchKernelGGL(pv_key_cache_probe_kernel, dim3((PV_NSEG * kw.seg_cap + PV_BLOCK - 1) / PV_BLOCK),
                                    dim3(PV_BLOCK), 0, stream, d_pk + 32 * c0,
-                                   kw, kcv);
+                                   kw, kcv, xtv);
                 PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
             }
             gate = Gate{kw.nkeys, kw.slot_req};
@@ -3819,11 +3846,12 @@ static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t 
             tev.push_back(e);
         }
     };
-    // the sub-batches share one set of comb tables: sub-batch 0 builds them, the later ones read them
-    // (the node-side key cache, when it holds keys, plays that role itself)
+    // the sub-batches share one set of comb tables: sub-batch 0 builds the tables of its comb keys that
+    // the node-side key cache does not hold, the later ones read the cache's for cached keys and the
+    // shared store's for the rest (pv_key_cache_probe_kernel's two views)
     static const bool share_env = env_int("PV_PIPE_SHARE", 1) != 0;
     const bool share = share_env && np > 1 && (c.path == PV_PATH_AUTO || c.path == PV_PATH_COMB) &&
-                       kc_view().hmask == 0 && ensure_xtab() == PV_OK;
+                       ensure_xtab() == PV_OK;
     auto run = [&]() -> int {
         tmark(cs);
         if (share) PV_HIP(hipMemsetAsync(c.xt.htab, 0xFF, PV_XT_HASH * 4, s), PV_ERR_LAUNCH);

@@ -158,6 +158,47 @@ def test_pipelined_shared_tables_with_one_off_keys(native, sodium):
         _check(got, want, ("one-off keys", path))
 
 
+def test_pipelined_partly_warm_cache(native, adv400k):
+    """a pipelined host call with half of its signers in the node-side key cache. The later
+    sub-batches look a key up in the node cache first and in the call's shared store next
+    (pv_key_cache_probe_kernel's two views), so the uncached signers' tables are built once per call, not
+    once per sub-batch (round 5 turned sharing off whenever the cache held a key). Verdicts are
+    libsodium's on AUTO and forced COMB; the call is no slower than with the cache empty."""
+    import time
+    blob, off, pks, want = adv400k
+    keys, counts = np.unique(pks, axis=0, return_counts=True)
+    signers = [bytes(k) for k, c in zip(keys, counts) if c >= 100]
+    assert len(signers) >= 1000
+    kc = native.KeyCache
+
+    def timed_calls():
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            got = native.verify_sm_batch(blob, off, pks)
+            ts.append(time.perf_counter() - t0)
+            _check(got, want, "partly warm")
+        return float(np.median(ts))
+
+    try:
+        kc.configure(2048)
+        native.verify_sm_batch(blob, off, pks)  # warm: staging sized
+        cold = timed_calls()
+        kc.put(signers[::2])
+        assert kc.stats()[0] == len(signers[::2])
+        for path in (native.PV_PATH_AUTO, native.PV_PATH_COMB):
+            native.set_path(path)
+            try:
+                _check(native.verify_sm_batch(blob, off, pks), want, ("partly warm", path))
+            finally:
+                native.set_path(native.PV_PATH_AUTO)
+        warm = timed_calls()
+        print("pipelined 400k call: cache empty %.2f ms, half the signers cached %.2f ms" % (1e3 * cold, 1e3 * warm))
+        assert warm < 1.25 * cold, (warm, cold)
+    finally:
+        kc.configure(0)
+
+
 def test_multi_gpu_two_or_more_devices(native, adv400k):
     L = native.lib()
     G = L.pv_device_count()
