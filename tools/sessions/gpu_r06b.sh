@@ -8,7 +8,7 @@ O=gpurun_out/r06b
 mkdir -p $O
 DS=/tmp/nym_ab.npz
 timeout -k 10 300 python3 tools/nym_workload.py --out $DS > /dev/null || exit $?
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_abi.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest tests/test_gpu_host_path.py tests/test_gpu_keycache.py tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_abi.py -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1 || exit $?
 AB_EXTRA="--no-config3" timeout -k 10 900 bash tools/ab_env.sh 3 "scan:" "scatter:PLENUM_AMD_LIB=variants/fork0/libplenum_verify.so" > $O/ab_fork.txt 2>&1 || exit $?
 for r in 1 2 3; do
   PLENUM_AMD_LIB=variants/clock/libplenum_verify.so timeout -k 10 120 python3 tools/clock_probe.py --dataset $DS --label w24 >> $O/clock.jsonl 2>> $O/clock.log || exit $?
