@@ -1674,9 +1674,17 @@ __global__ __launch_bounds__(64) void pv_key_chain_lp_kernel(const uint8_t* __re
 
 // Per (key, position in [lo, hi), block of 16 entries): the comb table rows. Grid-stride over
 // nkeys * (hi - lo) * 8 items.
+// Optional wave priority for the fill (A/B knob): it runs beside the request-order prep and is the
+// later of the two inputs of the comb kernel.
+#ifndef PV_FILL_PRIO
+#define PV_FILL_PRIO 0
+#endif
 __global__ __launch_bounds__(PV_BLOCK, PV_FILL_MINBLOCKS) void pv_key_fill_kernel(KeyWork kw, Gate gate, int lo,
                                                                                   int hi) {
     if (!gate.keyed() || gate.off() || kw.nkeys[PV_SPLIT_SPARSE]) return;
+#if PV_FILL_PRIO > 0
+    __builtin_amdgcn_s_setprio(PV_FILL_PRIO);
+#endif
     const uint32_t np = (uint32_t)(hi - lo);
     const uint32_t items = kw.nkeys[PV_SPLIT_COMB_KEYS] * np * PV_COMB_BLOCKS;
     for (uint32_t it = blockIdx.x * PV_BLOCK + threadIdx.x; it < items; it += gridDim.x * PV_BLOCK) {

@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--dataset", default=None)
     ap.add_argument("--seconds", type=float, default=2.5)
     ap.add_argument("--label", default="")
+    ap.add_argument("--ramp", action="store_true",
+                    help="from an idle GPU: the stamps of steps 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64 run back to "
+                         "back (a sync after each of those steps to read them): does the step time fall because "
+                         "the clock rises, or at the same clock?")
     a = ap.parse_args()
     if a.dataset and os.path.exists(a.dataset):
         blob, off, pks, _ = nym_workload.load(a.dataset)
@@ -39,6 +43,21 @@ def main():
     _native.ensure_device(0)
     L = _native.lib()
     db = bench.DeviceBatch(blob, off, pks)
+    if a.ramp:
+        _native.check(L.pv_sync(), "pv_sync")
+        time.sleep(2.0)  # idle first
+        marks = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64}
+        for step in range(1, 65):
+            t1 = time.perf_counter()
+            db.verify()
+            if step in marks:
+                _native.check(L.pv_sync(), "pv_sync")
+                wall = time.perf_counter() - t1
+                r = stamps(L, off)
+                r.update({"label": a.label, "step": step, "wall_ms_incl_sync": round(1e3 * wall, 3)})
+                print(json.dumps(r), flush=True)
+        db.free()
+        return
     for _ in range(5):
         db.verify()
     _native.check(L.pv_sync(), "pv_sync")
@@ -51,29 +70,34 @@ def main():
         el = time.perf_counter() - t0
         if el >= a.seconds:
             break
-    nblk = L.pv_test_clock_stamps(None, 0)
     out = {"label": a.label, "steps": steps, "seconds": round(el, 3), "ms_per_step": round(1e3 * el / steps, 4),
            "verifies_per_s": round((len(off) - 1) * steps / el, 1), "lib": os.path.basename(os.path.dirname(
                os.environ.get("PLENUM_AMD_LIB", "")) or "product")}
-    if nblk <= 0:
-        out["error"] = "no stamps: not a PV_CLOCK_PROBE build"
-    else:
-        grid = (len(off) - 1 + 255) // 256
-        k = min(nblk, grid)
-        buf = np.zeros(4 * k, np.uint64)
-        got = L.pv_test_clock_stamps(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), k)
-        st = buf[:4 * got].reshape(-1, 4).astype(np.float64)
-        dt, dr = st[:, 1] - st[:, 0], st[:, 3] - st[:, 2]
-        ok = (dr > 0) & (dt > 0)
-        ghz = dt[ok] / dr[ok] * 0.1  # 100 MHz realtime ticks -> GHz
-        span_us = (st[ok, 3].max() - st[ok, 2].min()) / 100.0
-        out.update({"workgroups": int(ok.sum()), "clock_ghz_median": round(float(np.median(ghz)), 4),
-                    "clock_ghz_p10": round(float(np.percentile(ghz, 10)), 4),
-                    "clock_ghz_p90": round(float(np.percentile(ghz, 90)), 4),
-                    "wg_us_median": round(float(np.median(dr[ok])) / 100.0, 2),
-                    "kernel_span_us_from_stamps": round(float(span_us), 1)})
+    out.update(stamps(L, off))
     db.free()
     print(json.dumps(out), flush=True)
+
+
+def stamps(L, off):
+    """Clock figures from the last comb_ab launch's stamps (diagnostic build), else an error entry."""
+    nblk = L.pv_test_clock_stamps(None, 0)
+    if nblk <= 0:
+        return {"error": "no stamps: not a PV_CLOCK_PROBE build"}
+    grid = (len(off) - 1 + 255) // 256
+    k = min(nblk, grid)
+    buf = np.zeros(4 * k, np.uint64)
+    got = L.pv_test_clock_stamps(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), k)
+    st = buf[:4 * got].reshape(-1, 4).astype(np.float64)
+    dt, dr = st[:, 1] - st[:, 0], st[:, 3] - st[:, 2]
+    ok = (dr > 0) & (dt > 0)
+    ghz = dt[ok] / dr[ok] * 0.1  # 100 MHz realtime ticks -> GHz
+    span_us = (st[ok, 3].max() - st[ok, 2].min()) / 100.0
+    return {"workgroups": int(ok.sum()), "clock_ghz_median": round(float(np.median(ghz)), 4),
+            "clock_ghz_p10": round(float(np.percentile(ghz, 10)), 4),
+            "clock_ghz_p90": round(float(np.percentile(ghz, 90)), 4),
+            "wg_us_median": round(float(np.median(dr[ok])) / 100.0, 2),
+            "wg_kcycles_median": round(float(np.median(dt[ok])) / 1e3, 1),
+            "kernel_span_us_from_stamps": round(float(span_us), 1)}
 
 
 if __name__ == "__main__":
