@@ -853,6 +853,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sustain-s", type=float, default=2.0,
+                    help="N = 1: seconds of back-to-back headline steps before the sustained_load sub-measurement "
+                         "(0: skip it)")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-straus", action="store_true", help="skip the secondary Straus-path measurement")
     ap.add_argument("--no-config3", action="store_true", help="skip the configs[2] (2 % adversarial) leg")
@@ -1001,6 +1004,25 @@ def main():
     result = assemble_result(world, n, args.steps, args.warmup, elapsed, stage_ms, chunks, comb, nkeys,
                              float(blob.nbytes) / n, ok_local, ok_all, per_gpu_fixed=bool(args.per_gpu),
                              fused=_native.comb_fused() and n / chunks > FUSED_MIN_REQ)
+    if world == 1 and args.sustain_s > 0:
+        # the same step under sustained load: the MI355X raises its clock over ~2 s of back-to-back
+        # launches (1.74-1.80 GHz in the first step after idle, ~2.0 after 10 steps, ~2.2 after 2.5 s:
+        # in-kernel s_memtime / s_memrealtime stamps, profiles/r06/clock/), so the headline's 5 warm-up +
+        # 20 timed steps run below the clock a continuously loaded verifier holds. Reported beside the
+        # headline, never as `value`
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.sustain_s:
+            for _ in range(20):
+                step()
+            _native.check(L.pv_sync(), "pv_sync")
+        els, _ = timed(args.steps, stages=False)
+        result["sustained_load"] = {
+            "value": round(n * world * args.steps / els, 1), "ms_per_step": round(1e3 * els / args.steps, 3),
+            "steps": args.steps, "after_s": round(time.perf_counter() - t0 - els, 2),
+            "verdicts_ok": bool(np.array_equal(bits(db.verdict_words(), n), want_local)),
+            "note": "the headline step timed again after ~%.1f s of back-to-back steps (the clock a continuously "
+                    "loaded GPU holds; the headline itself follows the driver's warm-up)" % args.sustain_s}
+        phases["sustained_load"] = time.perf_counter() - t0
     if world > 1:
         result["rccl"] = rccl_summary(world, *comm.rccl_ranks())
     if world > 1 and not args.no_host_path:

@@ -239,23 +239,33 @@ int pv_kernel_times(double* prep_ms, double* table_ms, double* msm_ms, int* laun
  * assigned is dropped. The benchmark's headline never configures it.
  *   pv_key_cache_configure(capacity)  allocate room for `capacity` keys (0 = free, disabled)
  *   pv_key_cache_put(pks, n)          host keys (n x 32 B): build and insert the missing ones, refresh
- *                                     the present ones; least recently put keys are evicted when full.
- *                                     Synchronous (a key table takes ~1 ms of chain latency; a batch of
- *                                     keys is built in parallel)
+ *                                     the present ones; when full, the least recently USED keys are
+ *                                     evicted (every launch stamps the cache slots it reads; the stamps
+ *                                     are folded into the LRU order before a put evicts). Synchronous: a
+ *                                     batch of keys is built in parallel, ~0.1 ms of GPU time per key with
+ *                                     the affine and radix-65536 rows (1,024 keys in 0.10-0.12 s)
  *   pv_key_cache_clear()              drop every key (capacity kept)
  *   pv_key_cache_enable(on)           whether launches consult the cache (default on)
  *   pv_key_cache_stats(size, cap)     keys held / capacity
  *   pv_key_cache_contains(pk)         1 if the 32-byte key is cached
- *   pv_key_cache_auto(min_seen)       automatic admission (0 = off, the default): pv_verify_batch calls
- *                                     of <= 4,096 requests count their keys (larger calls count a sample
- *                                     of 4,096: one request's key per block of ceil(n / 4,096)), and a key seen
- *                                     min_seen times within the counting window (the last ~32k distinct keys) is
- *                                     put into the cache right behind that batch on the engine stream
- *                                     -- the call waits only for its own verdicts, the table build
- *                                     (~1 ms) overlaps the caller's next steps and the next launch is
- *                                     ordered after it. A failed admission leaves the verdicts
- *                                     unchanged and the keys uncached. Verkeys come from NYM records
- *                                     (plenum/server/request_handlers/utils.py:30-39): signers repeat
+ *   pv_key_cache_auto(min_seen)       automatic admission (0 = off, the default): once a
+ *                                     pv_verify_batch call's verdicts are back, the keys of its requests
+ *                                     that VERIFIED are counted (every request of calls of <= 4,096
+ *                                     requests, a sample of 4,096 of larger ones: one request per block of
+ *                                     ceil(n / 4,096)); a request with a failing signature never counts,
+ *                                     so senders without valid signatures cannot make the node build
+ *                                     tables or evict its signers (plenum/server/client_authn.py:84-118:
+ *                                     every signature is untrusted input). A key verified min_seen times
+ *                                     within the counting window (the last ~32k distinct keys) is put
+ *                                     into the cache behind that batch on the engine stream: the call
+ *                                     returns with its verdicts, the build (~0.1 ms of GPU time per key)
+ *                                     overlaps the caller's next steps and the next launch is ordered
+ *                                     after it. The count table is keyed by a per-process random secret
+ *                                     with bounded probing (csrc/kc_admit.h); an evicted key, or one whose
+ *                                     admission failed, counts from zero again and is re-admitted on its
+ *                                     next min_seen verified appearances. A failed admission leaves the
+ *                                     verdicts unchanged and the keys uncached. Verkeys come from NYM
+ *                                     records (plenum/server/request_handlers/utils.py:30-39): signers repeat
  *   pv_key_cache_auto_stats(a, f)     keys admitted automatically / admissions that failed */
 int pv_key_cache_configure(uint32_t capacity);
 int pv_key_cache_put(const uint8_t* pks, uint64_t n);
