@@ -80,12 +80,41 @@ class DeviceBatch:
             self.L.pv_dev_free(p)
 
 
+def usable_cpus():
+    """(affinity, quota, usable): the CPUs in this process's affinity set, the cgroup CPU quota in CPUs
+    (cgroup v2 cpu.max or v1 cfs_quota_us / cfs_period_us; None = unlimited or unreadable), and the
+    number of threads that can actually run at once = min of the two. A GPU box shares its host with
+    other tenants: its affinity set can show the whole machine (256 CPUs) while the cgroup grants ~16,
+    and libsodium on 256 threads then runs SLOWER than on 16 (profiles/r06/mid/bench.json: 0.30 M/s on 256 threads against 0.50 M/s on 16)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except Exception:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except Exception:
+            pass
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return aff, quota, usable
+
+
 def cpu_baseline(blob, off, pks, sample, target_s=10.0, config3=None, share=16, share_s=5.0):
     """libsodium 1.0.18 crypto_sign_open (the reference's verifier) over the first `sample` requests of
-    the same workload, repeated until about `target_s` seconds have run, on EVERY host CPU this process
-    may run on (len(sched_getaffinity), SURVEY §8d(i): the host's nproc) -- `value` and `cores`; then
-    the same on `share` threads (the per-GPU share of the node's cores, 128 / 8 on the MI355X nodes)
-    for about `share_s` seconds -- `per_gpu_share`. The C oracle on one thread if libsodium is absent.
+    the same workload, repeated until about `target_s` seconds have run, on every host CPU this process
+    can use (the host's nproc = the affinity set, capped by the cgroup CPU quota when the
+    box grants fewer CPUs than it shows: usable_cpus) -- `value` and `cores`; when the affinity set is
+    larger than that, also on the whole affinity set (`all_affinity_threads`, oversubscribed); then on
+    `share` threads (the per-GPU share of the node's cores, 128 / 8 on the MI355X nodes) for about
+    `share_s` seconds -- `per_gpu_share`. The C oracle on one thread if libsodium is absent.
     With config3 = (blob, off, pks), also libsodium's per-record verdicts over that whole batch (one
     pass on every CPU, timed and returned): the reference outputs the config-3 leg's GPU verdicts are
     checked against."""
@@ -97,11 +126,11 @@ def cpu_baseline(blob, off, pks, sample, target_s=10.0, config3=None, share=16, 
     fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                    ctypes.c_uint64, ctypes.c_int]
     path = find_libsodium()
-    nproc = len(os.sched_getaffinity(0))
+    aff, quota, nproc = usable_cpus()
     use_sodium = path is not None
     if not use_sodium:
         sample = min(sample, 2000)
-        nproc = share = 1
+        aff = nproc = share = 1
     off_s = np.ascontiguousarray(off[:sample + 1])
 
     def run(threads, seconds):
@@ -126,8 +155,16 @@ def cpu_baseline(blob, off, pks, sample, target_s=10.0, config3=None, share=16, 
     out = {"value": round(sample * passes / dt, 1), "unit": "verifies/s", "cores": nproc,
            "kind": "reference" if use_sodium else "port",
            "sample": "%d passes over %d requests of the same synthetic NYM workload, crypto_sign_open on %d "
-                     "threads = every CPU in this process's affinity set (%s), %s" % (passes, sample, nproc, cpu_model, impl),
-           "cpu_model": cpu_model, "accepted": int(acc), "seconds": round(dt, 3)}
+                     "threads = every CPU this process can use (affinity set %d, cgroup quota %s) (%s), %s" % (
+                         passes, sample, nproc, aff, "none" if quota is None else "%.1f CPUs" % quota, cpu_model, impl),
+           "cpu_model": cpu_model, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+           "accepted": int(acc), "seconds": round(dt, 3)}
+    if aff != nproc:
+        ap_, aa, adt = run(aff, share_s)
+        out["all_affinity_threads"] = {"value": round(sample * ap_ / adt, 1), "cores": aff, "accepted": int(aa),
+                                       "seconds": round(adt, 3),
+                                       "note": "the same loop on every CPU of the affinity set: more threads than "
+                                               "the cgroup quota lets run at once"}
     share = min(share, nproc)
     if share != nproc:
         sp, sa, sdt = run(share, share_s)
@@ -419,8 +456,8 @@ def _config1_worker(_):
 
 
 def config1_legs(wire, share=16):
-    """configs[0] on one core, then on one forked process per CPU of this process's affinity set
-    (SURVEY §8d(i): the host's nproc) and on `share` processes (one GPU's share of the node's cores);
+    """configs[0] on one core, then on one forked process per CPU this process can use (usable_cpus:
+    SURVEY §8d(i)'s nproc, capped by the cgroup quota) and on `share` processes (one GPU's share of the node's cores);
     each process runs the same 10k requests with its own authenticators, aggregate = all requests /
     wall time. Runs before the GPU comes up."""
     import multiprocessing as mp
@@ -428,7 +465,7 @@ def config1_legs(wire, share=16):
     one = config1_python(wire)
     if one is None:
         return None
-    nproc = len(os.sched_getaffinity(0))
+    _, _, nproc = usable_cpus()
 
     def pool(procs):
         t0 = time.perf_counter()
