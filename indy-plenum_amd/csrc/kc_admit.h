@@ -57,7 +57,31 @@ class AdmitTableT {
     void reset() {
         if (!e_.empty()) memset(e_.data(), 0, e_.size() * sizeof(Entry));
         used_ = 0;
+        gen_++;
     }
+
+    // Read-only lookup (the engine runs it while the batch's kernels run, before the verdicts are
+    // known): the key's entry index, or -1 if it is not in the table. Nothing is inserted, so keys of
+    // requests that turn out not to verify never occupy the window.
+    int32_t find(const uint8_t key[32]) const {
+        if (e_.empty()) return -1;
+        uint64_t w[4];
+        memcpy(w, key, 32);
+        uint32_t h = slot_of(w);
+        for (uint32_t p = 0; p < MAX_PROBE; p++, h = (h + 1) & (H - 1)) {
+            const Entry& e = e_[h];
+            if (!e.used) return -1;
+            if (e.w[0] == w[0] && e.w[1] == w[1] && e.w[2] == w[2] && e.w[3] == w[3]) return (int32_t)h;
+        }
+        return -1;
+    }
+    // One verified appearance of the key find() located at `idx` (valid while generation() is
+    // unchanged): the same outcome count() would give.
+    Outcome bump_at(int32_t idx, uint32_t min_seen) {
+        probes_++;
+        return bump(e_[(uint32_t)idx], min_seen);
+    }
+    uint64_t generation() const { return gen_; }
 
     // One verified appearance of `key`. ADMIT: it has reached min_seen in this window now (it is
     // marked admitted); ALREADY: it was admitted before; COUNTED: below min_seen; DROPPED: its probe
@@ -129,7 +153,7 @@ class AdmitTableT {
     uint64_t mult_;
     std::vector<Entry> e_;
     uint32_t used_ = 0;
-    uint64_t probes_ = 0, dropped_ = 0;
+    uint64_t probes_ = 0, dropped_ = 0, gen_ = 0;
 };
 
 // 2^17 entries (5.2 MB, allocated on first use): windows of 32,768 distinct keys

@@ -3517,22 +3517,30 @@ static int pv_stage_to_device(uint8_t* d_dst, uint8_t* h_stage, const uint8_t* s
 #endif
 static int kc_put_locked(const uint8_t* pks, uint64_t n, bool async);
 // Automatic admission: count the VERIFIED appearances of this batch's keys (idx: the sampled requests,
-// or null for all n); the keys reaching auto_min appearances in the window are returned, at most kcap of them.
-// The verdicts are vb[i] & 1 (zero-copy verdict bytes) or bit i of hver (verdict words).
-static void kc_auto_count(const uint8_t* pk, const uint64_t* idx, uint64_t n, const uint8_t* vb, const uint64_t* hver,
-                          std::vector<uint8_t>& admit) {
+// or null for all n; pre: each one's entry located by kc_auto_locate while the kernels ran, or -1); the
+// keys reaching auto_min appearances in the window are returned, at most kcap of them. The verdicts are
+// vb[i] & 1 (zero-copy verdict bytes) or bit i of hver (verdict words).
+static void kc_auto_count(const uint8_t* pk, const uint64_t* idx, uint64_t n, const int32_t* pre, uint64_t gen,
+                          const uint8_t* vb, const uint64_t* hver, std::vector<uint8_t>& admit) {
     auto& k = g_ctx.kc;
     for (uint64_t j = 0; j < n; j++) {
         const uint64_t i = idx ? idx[j] : j;
         const bool ok = vb ? (vb[i] & 1u) != 0 : ((hver[i >> 6] >> (i & 63)) & 1u) != 0;
         if (!ok) continue;  // a key is never counted on the strength of a failing signature
-        if (k.seen.count(pk + 32 * i, k.auto_min) == pvhost::AdmitTable::ADMIT) {
+        const auto o = pre && pre[j] >= 0 && k.seen.generation() == gen ? k.seen.bump_at(pre[j], k.auto_min)
+                                                                         : k.seen.count(pk + 32 * i, k.auto_min);
+        if (o == pvhost::AdmitTable::ADMIT) {
             admit.insert(admit.end(), pk + 32 * i, pk + 32 * i + 32);
             if (admit.size() >= 32ull * g_ctx.kw.kcap) break;
         }
     }
 }
-
+// The counting side's read-only lookups, run while the batch's kernels run (the verdicts decide later
+// which of them count).
+static void kc_auto_locate(const uint8_t* pk, const uint64_t* idx, uint64_t n, std::vector<int32_t>& pre) {
+    pre.resize(n);
+    for (uint64_t j = 0; j < n; j++) pre[j] = g_ctx.kc.seen.find(pk + 32 * (idx ? idx[j] : j));
+}
 static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const uint8_t* pk, uint64_t* d_out,
                             uint64_t** dver_out, uint64_t** hver_out);
 
@@ -3947,20 +3955,28 @@ bool pv_spin_verdict_bytes(const uint8_t* vb, uint64_t n) {
 // the call does not wait for the build (the next launch is stream-ordered after it).
 int kc_auto_after_batch(const uint8_t* pk, uint64_t n, hipStream_t s, const uint8_t* vb, const uint64_t* hver) {
     auto& k = g_ctx.kc;
-    if (!(vb && pv_spin_verdict_bytes(vb, n))) PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
-    if (!(k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken)) return PV_OK;
-    std::vector<uint8_t> admit;
-    if (n <= PV_KC_AUTO_MAX_BATCH) {
-        kc_auto_count(pk, nullptr, n, vb, hver, admit);
-    } else {  // a large batch counts a sample: one request from each block of ceil(n / 4,096), at a
-              // hashed position in the block (a fixed stride would alias with periodic signer orders)
-        const uint64_t stride = (n + PV_KC_AUTO_MAX_BATCH - 1) / PV_KC_AUTO_MAX_BATCH;
-        std::vector<uint64_t> sample;
-        sample.reserve(n / stride + 1);
-        for (uint64_t b = 0, t = 0; b < n; b += stride, t++)
-            sample.push_back(b + ((t * 0x9E3779B97F4A7C15ull) >> 40) % std::min(stride, n - b));
-        kc_auto_count(pk, sample.data(), sample.size(), vb, hver, admit);
+    const bool on = k.auto_min > 0 && k.cap > 0 && k.enabled && !k.broken;
+    // the requests counted: all of a batch of <= 4,096, else a sample of one request from each block of
+    // ceil(n / 4,096), at a hashed position in the block (a fixed stride would alias with periodic
+    // signer orders); their table entries are located while the kernels still run
+    std::vector<uint64_t> sample;
+    std::vector<int32_t> pre;
+    uint64_t gen = 0;
+    if (on) {
+        if (n > PV_KC_AUTO_MAX_BATCH) {
+            const uint64_t stride = (n + PV_KC_AUTO_MAX_BATCH - 1) / PV_KC_AUTO_MAX_BATCH;
+            sample.reserve(n / stride + 1);
+            for (uint64_t b = 0, t = 0; b < n; b += stride, t++)
+                sample.push_back(b + ((t * 0x9E3779B97F4A7C15ull) >> 40) % std::min(stride, n - b));
+        }
+        gen = k.seen.generation();
+        kc_auto_locate(pk, sample.empty() ? nullptr : sample.data(), sample.empty() ? n : sample.size(), pre);
     }
+    if (!(vb && pv_spin_verdict_bytes(vb, n))) PV_HIP(hipStreamSynchronize(s), PV_ERR_LAUNCH);
+    if (!on) return PV_OK;
+    std::vector<uint8_t> admit;
+    kc_auto_count(pk, sample.empty() ? nullptr : sample.data(), sample.empty() ? n : sample.size(), pre.data(), gen,
+                  vb, hver, admit);
     if (admit.empty()) return PV_OK;
     const std::string err = g_err;
     if (kc_put_locked(admit.data(), admit.size() / 32, true) == PV_OK) {

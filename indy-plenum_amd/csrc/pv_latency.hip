@@ -81,7 +81,7 @@ __device__ __noinline__ LatK lat_hash_k_call(pv_sig_words in, uint64_t smlen, co
     pv_hash_k(o.k, in, smlen, LatMsg{ap, sh});
     return o;
 }
-__device__ __forceinline__ void lat_hash_k(uint32_t k[8], const pv_sig_words& in, uint64_t smlen, const LatMsg& mw) {
+[[maybe_unused]] __device__ __forceinline__ void lat_hash_k(uint32_t k[8], const pv_sig_words& in, uint64_t smlen, const LatMsg& mw) {
 #if PV_LAT_SHA_CALL
     const LatK o = lat_hash_k_call(in, smlen, mw.ap, mw.sh);
 #pragma unroll

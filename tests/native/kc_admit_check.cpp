@@ -117,6 +117,25 @@ int main() {
         for (size_t i = 0; i < seq.size(); i++) std::printf("%s%d", i ? ", " : "", seq[i]);
         std::printf("], ");
     }
+    // find / bump_at (the engine's lookups while the kernels run) give what count gives
+    {
+        pvhost::AdmitTable a, b;
+        std::mt19937_64 r(7);
+        std::vector<uint8_t> keys(32ull * 64);
+        for (auto& x : keys) x = (uint8_t)r();
+        int same = 1, absent_first = 1;
+        for (int pass = 0; pass < 4; pass++)
+            for (int j = 0; j < 64; j++) {
+                const uint8_t* k = &keys[32ull * ((j * 7 + pass) % 64)];
+                const int32_t at = b.find(k);
+                if (pass == 0 && j < 8 && at != -1) absent_first = 0;  // never inserted by find
+                const auto gen = b.generation();
+                const int ob = at >= 0 && b.generation() == gen ? b.bump_at(at, 3) : b.count(k, 3);
+                same &= ob == a.count(k, 3);
+            }
+        std::printf("\"find_bump\": {\"same_as_count\": %d, \"find_inserts_nothing\": %d, \"used\": %u}, ", same,
+                    absent_first, b.used());
+    }
     // window turnover
     {
         using Small = pvhost::AdmitTableT<10>;

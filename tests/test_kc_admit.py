@@ -76,6 +76,13 @@ def test_forget_allows_readmission(report):
     assert report["forget"] == [COUNTED, ADMIT, ALREADY, 1, 0, COUNTED, ADMIT, ADMIT]
 
 
+def test_find_then_bump_matches_count(report):
+    """The engine locates each request's entry while the kernels run (find: read-only) and bumps it
+    once the verdict is known (bump_at): the same outcomes as count(), and find inserts nothing."""
+    fb = report["find_bump"]
+    assert fb["same_as_count"] == 1 and fb["find_inserts_nothing"] == 1 and fb["used"] == 64
+
+
 def test_window_turnover(report):
     w = report["window"]
     assert w["used_full"] == w["window"]
