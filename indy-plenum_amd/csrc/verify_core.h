@@ -142,6 +142,36 @@ PV_HD void pv_add_a(ge_p1p1& r, const ge_p3& p, const ATab& atab, int e) {
     fe_sub(r.T, d, c);            // F
 }
 
+// acc = [e](table point) straight from the cached entry (Y+X, Y-X, 2Z, 2dT): the extended point
+// (2X : 2Y : 2Z : 2T) with 2T = 2dT / d -- one product, where adding the entry to the identity took an
+// addition and its conversion (8). X and Y carried (X is subtracted by the next addition).
+template <class ATab>
+PV_HD void pv_load_a_p3(ge_p3& r, const ATab& atab, int e) {
+    const int j = e < 0 ? -e : e;
+    const bool neg = e < 0;
+    fe ypx, ymx, t, invd;
+    uint32_t w[20];
+    atab.load_half(j, 0, w);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        ypx.v[i] = neg ? w[10 + i] : w[i];
+        ymx.v[i] = neg ? w[i] : w[10 + i];
+    }
+    fe_sub4p(t, ypx, ymx);        // the entry's Y-X is a sum of reduced values (ge_p3_to_cached)
+    fe_carry(r.X, t);             // 2X
+    fe_add(t, ypx, ymx);
+    fe_carry(r.Y, t);             // 2Y
+    atab.load_half(j, 1, w);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        r.Z.v[i] = w[i];          // 2Z
+        t.v[i] = w[10 + i];
+    }
+    fe_cneg(t, t, neg);
+    fe_const(invd, PV_INVD);
+    fe_mul(r.T, t, invd);         // 2T
+}
+
 // r = acc + [f]B (B-table entry in affine niels form, loaded in two parts like pv_add_a).
 template <class BTab>
 PV_HD void pv_add_b(ge_p1p1& r, const ge_p3& p, const BTab& btab, int f) {
@@ -246,11 +276,13 @@ PV_HD void pv_straus_a_xyz(fe& X, fe& Y, fe& Z, const ATab& atab, const Dig& dig
 // nw: windows (uniform across the wave on the device: the wave's maximum).
 // add_b(acc): acc += [k2 S mod L]B, in place (pv_msm_kernel: the wide fixed-base comb's niels additions
 // straight into the loop's point; pv_straus_ar_xyz: one cached addition of a point computed elsewhere).
+#ifndef PV_STRAUS_TOP_LOAD
+#define PV_STRAUS_TOP_LOAD 1  // the top window's A entry loaded as the starting point (0: added to the identity)
+#endif
 template <class ATab, class RTab, class Dig, class AddB>
 PV_HD void pv_straus_ar_xyz_addb(fe& X, fe& Y, fe& Z, const ATab& atab, const RTab& rtab, const Dig& dig, int nw,
                                  const AddB& add_b) {
     ge_p3 acc;
-    ge_p3_identity(acc);
     ge_p1p1 t;
     uint32_t w1 = 0, w2 = 0;
     for (int win = nw - 1; win >= 0; win--) {
@@ -259,16 +291,22 @@ PV_HD void pv_straus_ar_xyz_addb(fe& X, fe& Y, fe& Z, const ATab& atab, const RT
             w2 = dig.ek2(win >> 3);
         }
         const int e1 = pv_nibble(w1, win), e2 = pv_nibble(w2, win);
-        if (win != nw - 1) {
-            for (int j = 0; j < 3; j++) {
+        if (win != nw - 1 || !PV_STRAUS_TOP_LOAD) {
+            if (win != nw - 1) {
+                for (int j = 0; j < 3; j++) {
+                    ge_p2_dbl(t, X, Y, Z);
+                    ge_p1p1_to_p2(X, Y, Z, t);
+                }
                 ge_p2_dbl(t, X, Y, Z);
-                ge_p1p1_to_p2(X, Y, Z, t);
+                ge_p1p1_to_p3(acc, t);
+            } else {
+                ge_p3_identity(acc);
             }
-            ge_p2_dbl(t, X, Y, Z);
+            pv_add_a(t, acc, atab, e1);
             ge_p1p1_to_p3(acc, t);
+        } else {
+            pv_load_a_p3(acc, atab, e1);  // the top window starts from the A entry itself
         }
-        pv_add_a(t, acc, atab, e1);
-        ge_p1p1_to_p3(acc, t);
         pv_add_a(t, acc, rtab, e2);
         if (win > 0) ge_p1p1_to_p2(X, Y, Z, t);
     }
