@@ -74,7 +74,30 @@ PV_HD void ge_cached_load_words(ge_cached& c, const uint32_t w[40]) {
     }
 }
 
-// Build the 9-entry table of [j](-A), j = 0..8, in cached form (entry 0 = identity).
+// Build the 9-entry table of [j](-A), j = 0..8, in cached form (entry 0 = identity). PV_TABLE_DBL: the
+// even entries 2, 4, 6, 8 by doubling (4 S + 4 M) entries 1, 2, 3, 4 -- read back from the table as the
+// projective point (Y+X - (Y-X) : Y+X + (Y-X) : 2Z) = (2X : 2Y : 2Z) -- and the odd ones by one addition
+// (8 M) of entry 1: 3 additions and 4 doublings instead of 6 and 1.
+#ifndef PV_TABLE_DBL
+#define PV_TABLE_DBL 0  // measured slower: table stage 1.76 vs 1.71-1.73 ms (profiles/r06/ab/ab_straus_topload_tabdbl.txt)
+#endif
+// (2X : 2Y : 2Z) of a stored cached entry, X and Y carried (ge_p2_dbl takes reduced limbs)
+template <class ATab>
+PV_HD void pv_table_entry_p2(fe& X, fe& Y, fe& Z, const ATab& tab, int j) {
+    uint32_t w[40];
+    tab.load(j, w);
+    fe ypx, ymx, t;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        ypx.v[i] = w[i];
+        ymx.v[i] = w[10 + i];
+        Z.v[i] = w[20 + i];
+    }
+    fe_sub4p(t, ypx, ymx);  // Y-X is a sum of reduced values (ge_p3_to_cached)
+    fe_carry(X, t);
+    fe_add(t, ypx, ymx);
+    fe_carry(Y, t);
+}
 template <class ATab>
 PV_HD void pv_build_a_table(ATab& tab, const ge_p3& negA) {
     ge_cached c, c1;
@@ -92,6 +115,23 @@ PV_HD void pv_build_a_table(ATab& tab, const ge_p3& negA) {
     ge_p3_to_cached(c, cur);
     ge_cached_store_words(w, c);
     tab.store(2, w);
+#if PV_TABLE_DBL
+#pragma nounroll
+    for (int j = 3; j <= 7; j += 2) {
+        ge_add_cached(t, cur, c1);            // [j] = [j - 1] + [1]
+        ge_p1p1_to_p3(cur, t);
+        ge_p3_to_cached(c, cur);
+        ge_cached_store_words(w, c);
+        tab.store(j, w);
+        fe X, Y, Z;
+        pv_table_entry_p2(X, Y, Z, tab, (j + 1) / 2);
+        ge_p2_dbl(t, X, Y, Z);                // [j + 1] = 2 [(j + 1) / 2]
+        ge_p1p1_to_p3(cur, t);
+        ge_p3_to_cached(c, cur);
+        ge_cached_store_words(w, c);
+        tab.store(j + 1, w);
+    }
+#else
 #pragma nounroll
     for (int j = 3; j <= 8; j++) {
         ge_add_cached(t, cur, c1);
@@ -100,6 +140,7 @@ PV_HD void pv_build_a_table(ATab& tab, const ge_p3& negA) {
         ge_cached_store_words(w, c);
         tab.store(j, w);
     }
+#endif
 }
 
 // Signed digit i of the packed recodings: nibble i of ek (radix 16), byte i of fs (radix 256).
