@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--dataset", default=None)
     ap.add_argument("--seconds", type=float, default=2.5)
     ap.add_argument("--label", default="")
+    ap.add_argument("--dump", default=None, help="also save the last launch's per-workgroup stamps (npz)")
     ap.add_argument("--ramp", action="store_true",
                     help="from an idle GPU: the stamps of steps 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64 run back to "
                          "back (a sync after each of those steps to read them): does the step time fall because "
@@ -73,13 +74,15 @@ def main():
     out = {"label": a.label, "steps": steps, "seconds": round(el, 3), "ms_per_step": round(1e3 * el / steps, 4),
            "verifies_per_s": round((len(off) - 1) * steps / el, 1), "lib": os.path.basename(os.path.dirname(
                os.environ.get("PLENUM_AMD_LIB", "")) or "product")}
-    out.update(stamps(L, off))
+    out.update(stamps(L, off, a.dump))
     db.free()
     print(json.dumps(out), flush=True)
 
 
-def stamps(L, off):
-    """Clock figures from the last comb_ab launch's stamps (diagnostic build), else an error entry."""
+def stamps(L, off, dump=None):
+    """Clock figures from the last comb_ab launch's stamps (diagnostic build), else an error entry.
+    Also the launch's shape from the workgroups' start / end times (100 MHz ticks): span, the median
+    workgroup time, how long the first and last 5 % of workgroups took to start and to end."""
     nblk = L.pv_test_clock_stamps(None, 0)
     if nblk <= 0:
         return {"error": "no stamps: not a PV_CLOCK_PROBE build"}
@@ -92,7 +95,16 @@ def stamps(L, off):
     ok = (dr > 0) & (dt > 0)
     ghz = dt[ok] / dr[ok] * 0.1  # 100 MHz realtime ticks -> GHz
     span_us = (st[ok, 3].max() - st[ok, 2].min()) / 100.0
-    return {"workgroups": int(ok.sum()), "clock_ghz_median": round(float(np.median(ghz)), 4),
+    r0 = st[ok, 2] - st[ok, 2].min()
+    r1 = st[ok, 3] - st[ok, 2].min()
+    if dump:
+        np.savez(dump, t0=st[ok, 0], t1=st[ok, 1], r0=st[ok, 2], r1=st[ok, 3])
+    shape = {"start_us_p5_p50_p95_max": [round(float(np.percentile(r0, q)) / 100.0, 1) for q in (5, 50, 95, 100)],
+             "end_us_min_p5_p50_p95": [round(float(np.percentile(r1, q)) / 100.0, 1) for q in (0, 5, 50, 95)],
+             # workgroup-time over (1,024 concurrent workgroup slots x span): 4 waves / SIMD x 4 SIMDs x 256 CUs
+             # / 4 waves per workgroup
+             "slot_busy_fraction": round(float((r1 - r0).sum()) / (1024.0 * float(r1.max())), 4)}
+    return {"launch_shape": shape,"workgroups": int(ok.sum()), "clock_ghz_median": round(float(np.median(ghz)), 4),
             "clock_ghz_p10": round(float(np.percentile(ghz, 10)), 4),
             "clock_ghz_p90": round(float(np.percentile(ghz, 90)), 4),
             "wg_us_median": round(float(np.median(dr[ok])) / 100.0, 2),
