@@ -2290,6 +2290,9 @@ __device__ __forceinline__ void pv_clock_stamp(uint64_t& t, uint64_t& r) {
 }
 #endif
 
+#ifndef PV_COMB_AB_PRIO
+#define PV_COMB_AB_PRIO 0
+#endif
 template <int W>
 __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kernel(uint64_t n, Work wk, KeyWork kw,
                                                                                 const uint4* __restrict__ bcomb,
@@ -2306,7 +2309,13 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kern
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     ge_p3 acc;
     const uint4* wkey = pv_kw_rows(kw, i);
+#if PV_COMB_AB_PRIO  // A/B knob: the [S]B phase at a higher issue priority than the [k](-A) phase
+    __builtin_amdgcn_s_setprio(PV_COMB_AB_PRIO);
+#endif
     pv_comb_bw_acc<W>(acc, bcomb, wkey, dig, &stg[wv][0][0]);
+#if PV_COMB_AB_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (wkey)  // [k](-A) came from the key's wide rows in the same loop
         pv_comb_store_q(wk, kw, i, acc);
     else
