@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 DS=/tmp/nym_1m.npz
 timeout -k 10 300 python3 tools/nym_workload.py --out $DS || exit $?
-BENCH="python3 bench.py --dataset $DS --no-cpu-baseline --no-host-path --no-config3"
+BENCH="python3 bench.py --dataset $DS --no-cpu-baseline --no-host-path --no-config3 --sustain-s 0"
 echo "== kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- $BENCH > $OUT/bench_traced.json 2> $OUT/trace.log || exit $?
 PMCB="$BENCH --steps 3 --warmup 1"
