@@ -58,6 +58,35 @@ rel_b:
     return PyLong_FromLong(rc);
 }
 
+/* verify_one(pk, sm) -> rc < 0 (the library's error code) or the verdict (0 / 1): ONE (32-byte key,
+ * signature || message) pair from two bytes-like objects, with no arrays built around them -- the
+ * unbatched drop-in's verifySignature singleton (nacl_wrappers.py:232-242). */
+static PyObject* fc_verify_one(PyObject* self, PyObject* args) {
+    Py_buffer k, m;
+    int rc = -1;
+    (void)self;
+    if (!g_verify) {
+        PyErr_SetString(PyExc_RuntimeError, "_fastcall.bind() was not called");
+        return NULL;
+    }
+    if (!PyArg_ParseTuple(args, "y*y*", &k, &m)) return NULL;
+    if (k.len != 32) {
+        PyErr_SetString(PyExc_ValueError, "verify_one: the key must be 32 bytes");
+    } else {
+        static const uint8_t empty[1] = {0};
+        const uint64_t off[2] = {0, (uint64_t)m.len};
+        uint8_t bit = 0;
+        Py_BEGIN_ALLOW_THREADS
+        rc = g_verify(m.len ? (const uint8_t*)m.buf : empty, off, 1, (const uint8_t*)k.buf, &bit);
+        Py_END_ALLOW_THREADS
+        if (rc == 0) rc = bit & 1;
+    }
+    PyBuffer_Release(&m);
+    PyBuffer_Release(&k);
+    if (PyErr_Occurred()) return NULL;
+    return PyLong_FromLong(rc);
+}
+
 /* finish_single(verified, results, a, b, keys_hex, sig_lines, sig_off, pair_off, pair_name, names):
  * plenum_amd/wire.py's per-request finish of device-verified single-signature requests a..b-1, in
  * request order, as ReqAuthenticator.authenticate leaves them (plenum/server/req_authenticator.py:
@@ -159,6 +188,7 @@ r_kh:
 static PyMethodDef fc_methods[] = {
     {"bind", fc_bind, METH_VARARGS, "bind(address of pv_verify_batch)"},
     {"verify", fc_verify, METH_VARARGS, "verify(blob, offsets, pks, bits) -> pv_verify_batch's return code"},
+    {"verify_one", fc_verify_one, METH_VARARGS, "verify_one(pk, sm) -> error code < 0, or the verdict 0 / 1"},
     {"finish_single", fc_finish_single, METH_VARARGS,
      "finish_single(verified, results, a, b, keys_hex, sig_lines, sig_off, pair_off, pair_name, names)"},
     {NULL, NULL, 0, NULL}};

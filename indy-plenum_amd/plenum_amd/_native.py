@@ -217,6 +217,22 @@ def verify_sm_batch(blob, offsets, pks):
     return np.unpackbits(bits, count=n, bitorder="little").view(bool)
 
 
+def verify_one(pk, sm):
+    """crypto_sign_open verdict of ONE (32-byte key, sig || msg) pair: the unbatched drop-in's call
+    (Verifier.verify outside an authenticate_batch), without the arrays verify_sm_batch builds."""
+    if _device is None:
+        ensure_device()
+    fc = _fast if _fast is not None else _fastcall()
+    if fc and hasattr(fc, "verify_one"):
+        rc = fc.verify_one(pk, sm)
+        if rc < 0:
+            check(rc, "pv_verify_batch")
+        return bool(rc)
+    off = np.array([0, len(sm)], dtype=np.uint64)
+    return bool(verify_sm_batch(np.frombuffer(bytes(sm) or b"\0", dtype=np.uint8), off,
+                                np.frombuffer(bytes(pk), dtype=np.uint8))[0])
+
+
 PV_INJECT_STAGE = 1  # pv_test_inject: fail the next host-buffer stagings of a device
 
 

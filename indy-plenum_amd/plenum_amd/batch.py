@@ -106,4 +106,6 @@ def verdict(pk, sm):
         v = cache.get(pk, sm)
         if v is not None:
             return v
+    if engine is None:  # one launch of one pair, no arrays built around it
+        return _native.verify_one(pk, sm)
     return bool(verify_pairs([(pk, sm)], engine)[0])

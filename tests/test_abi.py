@@ -103,6 +103,10 @@ def test_fastcall_binding_matches_ctypes_entry(native):
             fc.verify(*bad)
     with pytest.raises((TypeError, BufferError)):
         fc.verify(blob, off, pks, bytes(1))                                 # read-only verdict buffer
+    # the one-pair call (the unbatched drop-in): the same entry point and return code
+    assert fc.verify_one(bytes(32), bytes(64)) == rc_c
+    with pytest.raises(ValueError):
+        fc.verify_one(bytes(31), bytes(64))                                 # short key
 
 
 def test_b58decode_batch_vs_restatement():

@@ -49,6 +49,28 @@ def test_golden_verdict_vectors_on_gpu(nat):
     nat.set_path(nat.PV_PATH_AUTO)
 
 
+def test_verify_one_golden_vectors(nat, sodium):
+    """The unbatched drop-in's one-pair call (_native.verify_one: _fastcall.verify_one, no arrays) on
+    the 220 committed libsodium vectors, an empty message and a 128 KiB one, and through
+    nacl_wrappers.Verifier outside any batch: libsodium's verdicts; a short key raises."""
+    from plenum_amd.nacl_wrappers import Verifier
+    with open(os.path.join(HERE, "golden", "verdicts.json")) as f:
+        vec = json.load(f)
+    for c in vec:
+        assert nat.verify_one(bytes.fromhex(c["pk"]), bytes.fromhex(c["sm"])) == c["ok"], c["cls"]
+    pk, sk = sodium.seed_keypair(b"\x07" * 32)
+    for m in (b"", bytes(range(256)) * 512):
+        sm = sodium.sign_detached(m, sk) + m
+        assert nat.verify_one(pk, sm) is True
+        assert Verifier(pk).verify(sm[:64], m) is True
+        bad = bytearray(sm)
+        bad[-1 if m else 0] ^= 1
+        assert nat.verify_one(pk, bytes(bad)) is False
+        assert Verifier(pk).verify(bytes(bad[:64]), bytes(bad[64:])) is False
+    with pytest.raises(ValueError):
+        nat.verify_one(pk[:31], sm)
+
+
 def test_long_messages_mixed_with_short(nat, sodium, oracle):
     g = VectorGen(sodium, oracle, seed=21)
     rng = np.random.default_rng(21)
