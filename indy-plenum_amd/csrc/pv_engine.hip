@@ -2340,6 +2340,9 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kern
 // chunks of >= PV_ENC16_MIN requests, else 8: at 1M requests 1,024 waves of 16 spend 0.185-0.190 ms
 // against 0.191-0.198 for 2,048 waves of 8 (profiles/r05/ab_encode_prefetch.txt); a smaller chunk has
 // fewer waves than SIMDs either way, and its encode then lasts one wave's chain, shorter with 8.
+#ifndef PV_ENC_SMALL_B
+#define PV_ENC_SMALL_B 8
+#endif
 #ifndef PV_ENC16_MIN
 #define PV_ENC16_MIN (1u << 20)
 #endif
@@ -2389,6 +2392,58 @@ struct DevEncSink {
         if (l == 0 && r0 < n) verdict[r0 >> 6] = bits;
     }
 };
+// The encode's one inversion per lane done by the whole wave (PV_ENC_WAVE_INV): the 64 lanes' products
+// are multiplied pairwise across lanes (xor partners 32, 16, 8, 4) down to four products, one per lane
+// residue mod 4; those four are inverted at once in limb-parallel form (lp_invert: row r = the product
+// of the lanes = r mod 4, a chain of ~265 limb-parallel products at ~300 cycles each) and the inverses
+// walked back up the same tree (one product per level). Where every lane ran its own ~27k-instruction
+// exponentiation chain (one wave per SIMD at 1M requests: the chain's latency was the kernel's time),
+// the wave now issues ~14k instructions on a chain ~2.5x shorter. Every lane of the wave must be active
+// (pv_encode_kernel: all lanes run the batch).
+#ifndef PV_ENC_WAVE_INV
+#define PV_ENC_WAVE_INV 1
+#endif
+__device__ __forceinline__ void pv_shfl_xor_fe(fe& o, const fe& a, int m) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) o.v[k] = __shfl_xor(a.v[k], m);
+}
+struct PvWaveInvert {
+    __device__ void operator()(fe& x) const {
+#if LP_DEVICE
+        const uint32_t lane = threadIdx.x & 63u;
+        constexpr int M[4] = {32, 16, 8, 4};
+        fe p[5], q;
+        p[0] = x;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            pv_shfl_xor_fe(q, p[i], M[i]);
+            fe_mul(p[i + 1], p[i], q);
+        }
+        // row r (lanes 16 r + k) gets limb k of lane r's product: the product of the lanes = r mod 4
+        const LpLane c = LpLane::make();
+        const int src = (int)(lane >> 4);
+        uint32_t z = 0;
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            const uint32_t t = __shfl(p[4].v[k], src);
+            z = (lane & 15u) == (uint32_t)k ? t : z;
+        }
+        const lu zi = lp_invert(c, lu(z));
+        fe inv;
+#pragma unroll
+        for (int k = 0; k < 10; k++) inv.v[k] = __shfl(static_cast<uint32_t>(zi), (int)(16u * (lane & 3u)) + k);
+#pragma unroll
+        for (int i = 3; i >= 0; i--) {
+            pv_shfl_xor_fe(q, p[i], M[i]);
+            fe_mul(inv, inv, q);
+        }
+        x = inv;
+#else
+        fe_invert(x, x);
+#endif
+    }
+};
+
 template <int B>
 __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* __restrict__ sm,
                                                                  const uint64_t* __restrict__ off, uint64_t n,
@@ -2405,8 +2460,13 @@ __global__ __launch_bounds__(PV_BLOCK, 2) void pv_encode_kernel(const uint8_t* _
         const uint32_t r = w * (64u * B) + l + 64 * t;
         use[t] = r < n && wk.flags[r < n ? r : 0] != 0;
     }
+#if PV_ENC_WAVE_INV
+    pv_encode_batch_stream_b<B>(src, use, DevEncSink<B>{sm, off, comb ? kw.sverdict : verdict,
+                                                        comb ? kw.slot_req : nullptr, w, l, n}, PvWaveInvert{});
+#else
     pv_encode_batch_stream_b<B>(src, use, DevEncSink<B>{sm, off, comb ? kw.sverdict : verdict,
                                                         comb ? kw.slot_req : nullptr, w, l, n});
+#endif
 }
 
 // ------------------------------------------------------------------------------------------ host
@@ -3019,8 +3079,8 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             hipLaunchKernelGGL(pv_encode_kernel<16>, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                            g_ctx.work, d_verdict + c0 / 64, kw, gate);
         } else {
-            const unsigned egrid = (unsigned)((m + PV_BLOCK * 8 - 1) / (PV_BLOCK * 8));
-            hipLaunchKernelGGL(pv_encode_kernel<8>, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
+            const unsigned egrid = (unsigned)((m + PV_BLOCK * PV_ENC_SMALL_B - 1) / (PV_BLOCK * PV_ENC_SMALL_B));
+            hipLaunchKernelGGL(pv_encode_kernel<PV_ENC_SMALL_B>, dim3(egrid), dim3(PV_BLOCK), 0, stream, d_sm, d_off + c0, m,
                            g_ctx.work, d_verdict + c0 / 64, kw, gate);
         }
         PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);

@@ -531,8 +531,13 @@ PV_HD void pv_encode_prefix(const Src& src, bool* use, fe* c, int t0) {
         else fe_mul(c[t], c[t - 1], z);
     }
 }
-template <int B, class Src, class Sink>
-PV_HD void pv_encode_batch_stream_b(const Src& src, bool use[B], const Sink& sink) {
+// The batch's one inversion: each lane inverts its own product (fe_invert), unless the caller passes a
+// wave-wide inverter (pv_engine.hip PvWaveInvert: every lane of the wave at once, limb-parallel).
+struct PvFeInvert {
+    PV_HD void operator()(fe& x) const { fe_invert(x, x); }
+};
+template <int B, class Src, class Sink, class Inv = PvFeInvert>
+PV_HD void pv_encode_batch_stream_b(const Src& src, bool use[B], const Sink& sink, const Inv& invert = Inv()) {
     static_assert(B == 16 || B <= 12, "pv_encode_batch_stream_b: 16, or one group of at most 12");
     if constexpr (B == 16) {
         // two groups of 8 under ONE inversion, holding one group's prefix products at a time: group 1's
@@ -546,7 +551,7 @@ PV_HD void pv_encode_batch_stream_b(const Src& src, bool use[B], const Sink& sin
         pv_encode_prefix<H>(src, use, c, 0);
         fe inv, inv0, inv1;
         fe_mul(inv, c[H - 1], p1);
-        fe_invert(inv, inv);
+        invert(inv);
         fe_mul(inv0, inv, p1);
         fe_mul(inv1, inv, c[H - 1]);
         pv_encode_group<H>(src, use, sink, c, inv0, 0);
@@ -556,7 +561,8 @@ PV_HD void pv_encode_batch_stream_b(const Src& src, bool use[B], const Sink& sin
         fe c[B];
         pv_encode_prefix<B>(src, use, c, 0);
         fe inv;
-        fe_invert(inv, c[B - 1]);
+        fe_copy(inv, c[B - 1]);
+        invert(inv);
         pv_encode_group<B>(src, use, sink, c, inv, 0);
     }
 }

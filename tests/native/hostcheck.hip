@@ -653,6 +653,10 @@ void hc_lp_pow22523(uint32_t* h, const uint32_t* f) {
     const LpLane c = LpLane::make();
     hc_rows_out(h, lp_pow22523(c, hc_rows_in(f)));
 }
+void hc_lp_invert(uint32_t* h, const uint32_t* f) {
+    const LpLane c = LpLane::make();
+    hc_rows_out(h, lp_invert(c, hc_rows_in(f)));
+}
 // lp_mul_dual / lp_pow22523<true>: rows 2, 3 of the inputs must repeat rows 0, 1
 void hc_lp_mul_dual(uint32_t* h, const uint32_t* f, const uint32_t* g) {
     const LpLane c = LpLane::make();

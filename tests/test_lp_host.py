@@ -70,6 +70,24 @@ def test_lp_pow22523(hc):
             assert from_limbs(hr) % P == pow(z[r], (P - 5) // 8, P)
 
 
+def test_lp_invert(hc):
+    """lp_invert (the encode kernel's wave-wide inversion, pv_wave_invert): 1 / z in every row, for
+    reduced inputs and for limbs at the lp_mul output bound."""
+    rng = random.Random(41)
+    h = A40()
+    for it in range(6):
+        if it < 4:
+            z = [rng.randrange(1, P) for _ in range(4)]
+            hc.hc_lp_invert(h, rows_in(z))
+        else:  # unreduced limbs as the products that feed it leave them (< 2^26 + 2^23)
+            limbs = [rand_limbs(rng, 26.1) for _ in range(4)]
+            z = [from_limbs(l) % P or 1 for l in limbs]
+            arr = A40(*[v for l in limbs for v in l])
+            hc.hc_lp_invert(h, arr)
+        for r, hr in enumerate(rows_out(h)):
+            assert from_limbs(hr) % P == pow(z[r], P - 2, P), (it, r)
+
+
 def test_lp_mul_dual_matches_lp_mul(hc):
     """lp_mul_dual (the decompression chain's product: rows 0, 1 sum column terms 0..4, rows 2, 3 terms
     5..9 on operands pre-rotated by five limbs, halves added across with v_permlane32_swap) gives
