@@ -420,31 +420,33 @@ LP_FN lu lp_pow22523(const LpLane& c, const lu& z) {
 }
 
 // z^(p - 2) = 1 / z in every row at once (fe_invert's chain: z^(2^250 - 1), five squarings, times
-// z^11). The encode kernel inverts one cross-lane product per row with it (pv_wave_invert): a chain of
-// limb-parallel products, ~300 cycles each, instead of each lane's own chain of 101-instruction squarings.
+// z^11). The encode kernel inverts the wave's cross-lane products with it (pv_engine.hip PvWaveInvert):
+// a chain of limb-parallel products, ~300 cycles each (fewer with DUAL: two values, five column terms
+// per lane), instead of each lane's own chain of 101-instruction squarings.
+template <bool DUAL = false>
 LP_FN lu lp_invert(const LpLane& c, const lu& z) {
-    lu t0 = lp_sq(c, z);                          // z^2
-    lu t1 = lp_sqn(c, t0, 2);                     // z^8
-    t1 = lp_mul(c, z, t1);                        // z^9
-    t0 = lp_mul(c, t0, t1);                       // z^11
-    lu t2 = lp_sq(c, t0);                         // z^22
-    t1 = lp_mul(c, t1, t2);                       // z^(2^5 - 1)
-    t2 = lp_sqn(c, t1, 5);
-    t1 = lp_mul(c, t2, t1);                       // z^(2^10 - 1)
-    t2 = lp_sqn(c, t1, 10);
-    t2 = lp_mul(c, t2, t1);                       // z^(2^20 - 1)
-    lu t3 = lp_sqn(c, t2, 20);
-    t2 = lp_mul(c, t3, t2);                       // z^(2^40 - 1)
-    t2 = lp_sqn(c, t2, 10);
-    t1 = lp_mul(c, t2, t1);                       // z^(2^50 - 1)
-    t2 = lp_sqn(c, t1, 50);
-    t2 = lp_mul(c, t2, t1);                       // z^(2^100 - 1)
-    t3 = lp_sqn(c, t2, 100);
-    t2 = lp_mul(c, t3, t2);                       // z^(2^200 - 1)
-    t2 = lp_sqn(c, t2, 50);
-    t1 = lp_mul(c, t2, t1);                       // z^(2^250 - 1)
-    t1 = lp_sqn(c, t1, 5);                        // z^(2^255 - 32)
-    return lp_mul(c, t1, t0);                     // z^(2^255 - 21)
+    lu t0 = lp_mulx<DUAL>(c, z, z);               // z^2
+    lu t1 = lp_sqn<DUAL>(c, t0, 2);               // z^8
+    t1 = lp_mulx<DUAL>(c, z, t1);                 // z^9
+    t0 = lp_mulx<DUAL>(c, t0, t1);                // z^11
+    lu t2 = lp_mulx<DUAL>(c, t0, t0);             // z^22
+    t1 = lp_mulx<DUAL>(c, t1, t2);                // z^(2^5 - 1)
+    t2 = lp_sqn<DUAL>(c, t1, 5);
+    t1 = lp_mulx<DUAL>(c, t2, t1);                // z^(2^10 - 1)
+    t2 = lp_sqn<DUAL>(c, t1, 10);
+    t2 = lp_mulx<DUAL>(c, t2, t1);                // z^(2^20 - 1)
+    lu t3 = lp_sqn<DUAL>(c, t2, 20);
+    t2 = lp_mulx<DUAL>(c, t3, t2);                // z^(2^40 - 1)
+    t2 = lp_sqn<DUAL>(c, t2, 10);
+    t1 = lp_mulx<DUAL>(c, t2, t1);                // z^(2^50 - 1)
+    t2 = lp_sqn<DUAL>(c, t1, 50);
+    t2 = lp_mulx<DUAL>(c, t2, t1);                // z^(2^100 - 1)
+    t3 = lp_sqn<DUAL>(c, t2, 100);
+    t2 = lp_mulx<DUAL>(c, t3, t2);                // z^(2^200 - 1)
+    t2 = lp_sqn<DUAL>(c, t2, 50);
+    t1 = lp_mulx<DUAL>(c, t2, t1);                // z^(2^250 - 1)
+    t1 = lp_sqn<DUAL>(c, t1, 5);                  // z^(2^255 - 32)
+    return lp_mulx<DUAL>(c, t1, t0);              // z^(2^255 - 21)
 }
 
 // The 10 limbs of row r as a scalar fe (uniform values: v_readlane).

@@ -2337,14 +2337,15 @@ __global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kern
 // per request group. Wave w covers requests [64 B w, 64 B (w + 1)): lane l handles 64 B w + l + 64 t,
 // t = 0..B-1, so every load is coalesced and group t's ballot is verdict word B w + t. Points are
 // re-read from q rather than held. B = 16 (two groups of 8 under one inversion, verify_core.h) for
-// chunks of >= PV_ENC16_MIN requests, else 8: at 1M requests 1,024 waves of 16 spend 0.185-0.190 ms
-// against 0.191-0.198 for 2,048 waves of 8 (profiles/r05/ab_encode_prefetch.txt); a smaller chunk has
-// fewer waves than SIMDs either way, and its encode then lasts one wave's chain, shorter with 8.
+// chunks of >= PV_ENC16_MIN requests, else PV_ENC_SMALL_B = 8. With each lane's own inversion chain 16
+// won at 1M requests (0.185-0.190 ms against 0.191-0.198 for 2,048 waves of 8, profiles/r05/
+// ab_encode_prefetch.txt); with the wave's limb-parallel inversion 8 wins everywhere (0.145-0.148 vs
+// 0.159-0.161 ms at 1M, 4 per lane 0.185-0.191: profiles/r06/ab/ab_encode_batch.txt), so 16 is off.
 #ifndef PV_ENC_SMALL_B
 #define PV_ENC_SMALL_B 8
 #endif
 #ifndef PV_ENC16_MIN
-#define PV_ENC16_MIN (1u << 20)
+#define PV_ENC16_MIN 0xffffffffu
 #endif
 template <int B>
 struct DevEncSrc {
@@ -2393,15 +2394,18 @@ struct DevEncSink {
     }
 };
 // The encode's one inversion per lane done by the whole wave (PV_ENC_WAVE_INV): the 64 lanes' products
-// are multiplied pairwise across lanes (xor partners 32, 16, 8, 4) down to four products, one per lane
-// residue mod 4; those four are inverted at once in limb-parallel form (lp_invert: row r = the product
-// of the lanes = r mod 4, a chain of ~265 limb-parallel products at ~300 cycles each) and the inverses
-// walked back up the same tree (one product per level). Where every lane ran its own ~27k-instruction
-// exponentiation chain (one wave per SIMD at 1M requests: the chain's latency was the kernel's time),
-// the wave now issues ~14k instructions on a chain ~2.5x shorter. Every lane of the wave must be active
-// (pv_encode_kernel: all lanes run the batch).
+// are multiplied pairwise across lanes (xor partners 32, 16, 8, 4, and 2 with PV_ENC_INV_DUAL) down to
+// four products, one per lane residue mod 4 (two, mod 2), which are inverted at once in limb-parallel form
+// (lp_invert: row r = the product of the lanes = r mod 4; DUAL: rows 0, 1 the two products, repeated in
+// rows 2, 3, and five column terms per lane, a shorter dependent chain per product), and the inverses
+// walked back down the same tree (one product per level). Where every lane ran its own ~27k-instruction
+// exponentiation chain (the chain's latency was most of the kernel's time), the wave now runs ~265
+// limb-parallel products. Every lane of the wave must be active (pv_encode_kernel: all lanes run the batch).
 #ifndef PV_ENC_WAVE_INV
 #define PV_ENC_WAVE_INV 1
+#endif
+#ifndef PV_ENC_INV_DUAL
+#define PV_ENC_INV_DUAL 1
 #endif
 __device__ __forceinline__ void pv_shfl_xor_fe(fe& o, const fe& a, int m) {
 #pragma unroll
@@ -2410,30 +2414,32 @@ __device__ __forceinline__ void pv_shfl_xor_fe(fe& o, const fe& a, int m) {
 struct PvWaveInvert {
     __device__ void operator()(fe& x) const {
 #if LP_DEVICE
+        constexpr int LV = PV_ENC_INV_DUAL ? 5 : 4;  // tree levels
+        constexpr uint32_t RES = PV_ENC_INV_DUAL ? 1u : 3u;  // lane residue a row's product covers
         const uint32_t lane = threadIdx.x & 63u;
-        constexpr int M[4] = {32, 16, 8, 4};
-        fe p[5], q;
+        constexpr int M[5] = {32, 16, 8, 4, 2};
+        fe p[LV + 1], q;
         p[0] = x;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < LV; i++) {
             pv_shfl_xor_fe(q, p[i], M[i]);
             fe_mul(p[i + 1], p[i], q);
         }
-        // row r (lanes 16 r + k) gets limb k of lane r's product: the product of the lanes = r mod 4
+        // row r (lanes 16 r + k) gets limb k of lane (r & RES)'s product
         const LpLane c = LpLane::make();
-        const int src = (int)(lane >> 4);
+        const int src = (int)((lane >> 4) & RES);
         uint32_t z = 0;
 #pragma unroll
         for (int k = 0; k < 10; k++) {
-            const uint32_t t = __shfl(p[4].v[k], src);
+            const uint32_t t = __shfl(p[LV].v[k], src);
             z = (lane & 15u) == (uint32_t)k ? t : z;
         }
-        const lu zi = lp_invert(c, lu(z));
+        const lu zi = lp_invert<PV_ENC_INV_DUAL != 0>(c, lu(z));
         fe inv;
 #pragma unroll
-        for (int k = 0; k < 10; k++) inv.v[k] = __shfl(static_cast<uint32_t>(zi), (int)(16u * (lane & 3u)) + k);
+        for (int k = 0; k < 10; k++) inv.v[k] = __shfl(static_cast<uint32_t>(zi), (int)(16u * (lane & RES)) + k);
 #pragma unroll
-        for (int i = 3; i >= 0; i--) {
+        for (int i = LV - 1; i >= 0; i--) {
             pv_shfl_xor_fe(q, p[i], M[i]);
             fe_mul(inv, inv, q);
         }

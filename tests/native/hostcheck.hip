@@ -662,6 +662,10 @@ void hc_lp_mul_dual(uint32_t* h, const uint32_t* f, const uint32_t* g) {
     const LpLane c = LpLane::make();
     hc_rows_out(h, lp_mul_dual(c, hc_rows_in(f), hc_rows_in(g)));
 }
+void hc_lp_invert_dual(uint32_t* h, const uint32_t* f) {
+    const LpLane c = LpLane::make();
+    hc_rows_out(h, lp_invert<true>(c, hc_rows_in(f)));
+}
 void hc_lp_pow22523_dual(uint32_t* h, const uint32_t* f) {
     const LpLane c = LpLane::make();
     hc_rows_out(h, lp_pow22523<true>(c, hc_rows_in(f)));

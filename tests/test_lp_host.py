@@ -71,7 +71,7 @@ def test_lp_pow22523(hc):
 
 
 def test_lp_invert(hc):
-    """lp_invert (the encode kernel's wave-wide inversion, pv_wave_invert): 1 / z in every row, for
+    """lp_invert (the encode kernel's wave-wide inversion, PvWaveInvert): 1 / z in every row, for
     reduced inputs and for limbs at the lp_mul output bound."""
     rng = random.Random(41)
     h = A40()
@@ -86,6 +86,23 @@ def test_lp_invert(hc):
             hc.hc_lp_invert(h, arr)
         for r, hr in enumerate(rows_out(h)):
             assert from_limbs(hr) % P == pow(z[r], P - 2, P), (it, r)
+
+
+def test_lp_invert_dual(hc):
+    """lp_invert<true> (the encode's default, PV_ENC_INV_DUAL): two values in rows 0, 1, repeated in
+    rows 2, 3 (the wave tree's two products), 1 / z in every row."""
+    rng = random.Random(43)
+    h = A40()
+    for it in range(4):
+        if it < 3:
+            z = [rng.randrange(1, P) for _ in range(2)]
+            hc.hc_lp_invert_dual(h, rows_in(z + z))
+        else:
+            limbs = [rand_limbs(rng, 26.1) for _ in range(2)]
+            z = [from_limbs(l) % P or 1 for l in limbs]
+            hc.hc_lp_invert_dual(h, A40(*[v for l in limbs + limbs for v in l]))
+        for r, hr in enumerate(rows_out(h)):
+            assert from_limbs(hr) % P == pow(z[r & 1], P - 2, P), (it, r)
 
 
 def test_lp_mul_dual_matches_lp_mul(hc):
