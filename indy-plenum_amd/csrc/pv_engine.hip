@@ -2293,18 +2293,25 @@ __device__ __forceinline__ void pv_clock_stamp(uint64_t& t, uint64_t& r) {
 #ifndef PV_COMB_AB_PRIO
 #define PV_COMB_AB_PRIO 0
 #endif
+// Workgroup size of the fused comb kernel (A/B knob): its waves share nothing (each stages its own
+// rows in its own 10 KB of LDS), so one-wave workgroups release a slot per wave instead of per four.
+// Measured: 64 within noise of 256, 128 3 % slower (profiles/r06/ab/ab_comb_ab_block.txt); 256 kept.
+#ifndef PV_COMB_AB_BLOCK
+#define PV_COMB_AB_BLOCK PV_BLOCK
+#endif
 template <int W>
-__global__ __launch_bounds__(PV_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kernel(uint64_t n, Work wk, KeyWork kw,
-                                                                                const uint4* __restrict__ bcomb,
-                                                                                Gate gate) {
+__global__ __launch_bounds__(PV_COMB_AB_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb_ab_kernel(uint64_t n, Work wk,
+                                                                                        KeyWork kw,
+                                                                                        const uint4* __restrict__ bcomb,
+                                                                                        Gate gate) {
     if (!gate.keyed() || gate.off()) return;
-    const uint32_t i = pv_xcd_block() * PV_BLOCK + threadIdx.x;  // slot
+    const uint32_t i = pv_xcd_block() * PV_COMB_AB_BLOCK + threadIdx.x;  // slot
     if (i >= gate.ncomb()) return;
 #if PV_CLOCK_PROBE
     uint64_t t0 = 0, r0 = 0;
     pv_clock_stamp(t0, r0);
 #endif
-    __shared__ uint4 stg[PV_BLOCK / 64][10][64];
+    __shared__ uint4 stg[PV_COMB_AB_BLOCK / 64][10][64];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const DevDigits dig{wk.digits, (uint32_t)wk.stride, i};
     ge_p3 acc;
@@ -3049,8 +3056,8 @@ int launch_chunk(int c, uint64_t n, const uint8_t* d_sm, const uint64_t* d_off, 
             PV_HIP(hipStreamWaitEvent(stream, g_ctx.ev_tables_ready, 0), PV_ERR_LAUNCH);
             if ((rc = mark(PV_STAGE_MSM))) return rc;
             if (fused)  // [S]B + [k](-A) in one kernel as soon as the tables are built
-                PV_LAUNCH_BC2(pv_comb_ab_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, g_ctx.d_bc2,
-                              gate);
+                PV_LAUNCH_BC2(pv_comb_ab_kernel, dim3((unsigned)((m + PV_COMB_AB_BLOCK - 1) / PV_COMB_AB_BLOCK)),
+                              dim3(PV_COMB_AB_BLOCK), 0, stream, m, g_ctx.work, kw, g_ctx.d_bc2, gate);
             else
                 hipLaunchKernelGGL(pv_comb_a_kernel, dim3(grid), dim3(PV_BLOCK), 0, stream, m, g_ctx.work, kw, gate);
             PV_HIP(hipGetLastError(), PV_ERR_LAUNCH);
