@@ -20,7 +20,7 @@ from plenum_amd import wire
 
 @pytest.fixture
 def cpu_engine(sodium, monkeypatch):
-    calls = {"ingress": 0, "sm": 0}
+    calls = {"ingress": 0, "sm": 0, "one": 0}
 
     def ingress(sb, so, mblob, moff, msg_idx, signer_idx, ib, io, vb, vo, vp):
         calls["ingress"] += 1
@@ -48,6 +48,12 @@ def cpu_engine(sodium, monkeypatch):
 
     monkeypatch.setattr(_native, "ingress_verify_arrays", ingress)
     monkeypatch.setattr(_native, "verify_sm_batch", sm_batch)
+    # the unbatched per-call path (batch.verdict without a batch context) of the sequential reference
+    def one(pk, sm):
+        calls["one"] += 1
+        return bool(sodium.sign_open_ok(bytes(sm), bytes(pk)))
+
+    monkeypatch.setattr(_native, "verify_one", one)
     return calls
 
 
@@ -165,11 +171,12 @@ def test_config1_sequential_and_wire_batch_agree(cpu_engine, sodium):
     with batch.active(batch.VerdictCache()):
         want = sequential(ra_seq, raws)
     assert all(r == {pool[i % len(pool)]["did"]} for i, (_, r) in enumerate(want))
-    assert cpu_engine["sm"] == k and cpu_engine["ingress"] == 0
+    # one unbatched verify per signature (batch.verdict -> _native.verify_one), no array launch
+    assert cpu_engine["one"] == k and cpu_engine["sm"] == 0 and cpu_engine["ingress"] == 0
     got = wire.authenticate_wire_batch(ra_wire, raws)
     assert [norm(r) for r in got] == [norm(r) for r in want]
     assert ra_wire._verified_reqs == ra_seq._verified_reqs
-    assert cpu_engine["ingress"] == 1 and cpu_engine["sm"] == k
+    assert cpu_engine["ingress"] == 1 and cpu_engine["sm"] == 0 and cpu_engine["one"] == k
 
 
 @pytest.mark.parametrize("raw", [b'{"a": 1}', b' {"a": 1}', b'{"a": 1} ', b'{"a": 1}\n', b'\xef\xbb\xbf{"a": 1}',
