@@ -3,10 +3,11 @@
 set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp
-O=gpurun_out/r06end
+TAG=${TAG:-r06end}
+O=gpurun_out/$TAG
 mkdir -p $O
 echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null) nproc: $(nproc)" > $O/host_cpus.txt
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1 || exit $?
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit $?
 timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.log || exit $?
-timeout -k 10 900 bash tools/profile_round.sh r06end > $O/profile.log 2>&1 || exit $?
+timeout -k 10 900 bash tools/profile_round.sh $TAG > $O/profile.log 2>&1 || exit $?
