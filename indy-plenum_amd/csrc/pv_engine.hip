@@ -3753,6 +3753,9 @@ int pv_verify_batch(const uint8_t* sm, const uint64_t* sm_off, uint64_t n, const
 #ifndef PV_PIPE_SUB
 #define PV_PIPE_SUB 262144
 #endif
+#ifndef PV_PIPE_END_DEFAULT
+#define PV_PIPE_END_DEFAULT (PV_PIPE_SUB / 2)
+#endif
 static constexpr uint64_t PV_PIPE_MAX = 64;                // sub-batches per call (copy events)
 static constexpr uint64_t PV_PIPE_MIN_BLOB = 8ull << 20;   // smaller blobs: one piece
 static uint64_t pipe_sub() {
@@ -3828,8 +3831,13 @@ static int stage_and_launch(const uint8_t* sm, const uint64_t* sm_off, uint64_t 
     // (profiles/r05/host_path: 1M requests, 0.5 + 3 x 1 + 0.5 of 262,144)
     std::vector<uint64_t> bnd{0};
     static const bool halves = env_int("PV_PIPE_HALF_ENDS", 1) != 0;
+    // first / last piece size (env PV_PIPE_END, A/B): half a sub-batch by default. Smaller ends are slower
+    // (1M arena: 116.8-119.1 M/s at 131,072, 113.6-114.1 at 65,536, 110.4-112.7 at 32,768; profiles/r06/
+    // host_path/ab_pipe_end.txt): the copies are the critical path and a sub-batch's kernels beside a DMA
+    // take longer than a small last piece's copy, so the last FULL piece's kernels become the tail
+    static const uint64_t end_req = (uint64_t)std::max(8192, env_int("PV_PIPE_END", (int)(PV_PIPE_END_DEFAULT)));
     if (blob >= PV_PIPE_MIN_BLOB && halves && n >= 3 * sub) {
-        const uint64_t h = sub / 2 / 64 * 64;
+        const uint64_t h = std::min<uint64_t>(end_req, sub) / 64 * 64;
         const uint64_t mid = n - 2 * h;
         const uint64_t k = std::min<uint64_t>(PV_PIPE_MAX - 2, std::max<uint64_t>(1, (mid + sub / 2) / sub));
         bnd.push_back(h);
