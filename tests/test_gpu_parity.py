@@ -181,3 +181,16 @@ def test_small_calls_long_records(native, sodium, oracle):
         got = native.verify_sm_batch(blob2, off + lead, pks)
         assert np.array_equal(got, want), (lead, np.nonzero(got != want)[0][:8])
         assert not native.last_zero_copy()
+
+
+def test_encode_wave_edges(native, sodium, oracle):
+    """Batch sizes at the encode kernel's wave edges (8 points per lane, 512 requests per wave, the wave's
+    64 lane products inverted together: PvWaveInvert), with lanes and whole groups past the batch's end and
+    rejected records (whose points are left out of the products) on both sides of each edge."""
+    g = VectorGen(sodium, oracle, seed=20)
+    cases = g.batch(2113, adversarial_frac=0.1)
+    want = reference_verdicts(sodium, cases)
+    for n in (448, 449, 1023, 1024, 1025, 1537, 2048, 2113):
+        blob, off, pks = pack(cases[:n])
+        got = native.verify_sm_batch(blob, off, pks)
+        assert np.array_equal(got, want[:n]), (n, np.nonzero(got != want[:n])[0][:10])
