@@ -617,6 +617,19 @@ class Comm:
             os.remove(self.path)
 
 
+def hbm_in_use():
+    """(bytes in use, total) on this process's current HIP device (hipMemGetInfo from the HIP runtime the
+    engine already loaded; device-wide, so other processes' allocations on the GPU count too), or None."""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        free, total = ctypes.c_size_t(), ctypes.c_size_t()
+        if hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) != 0:
+            return None
+        return total.value - free.value, total.value
+    except OSError:
+        return None
+
+
 def rccl_summary(world, nranks_by_rank, user_rank_by_rank):
     """The N > 1 line's `rccl` object: what RCCL itself reported on every rank (ncclCommCount /
     ncclCommUserRank through pv_comm_count), so the line shows the all-gather ran over `world` ranks."""
@@ -991,6 +1004,7 @@ def main():
     _native.ensure_device(local_rank)
     L = _native.lib()
     phases["pv_init"] = time.perf_counter() - t0
+    hbm_ctx = hbm_in_use()  # the engine context: fixed-base comb, workspace, staging
     log("rank %d: device %d up (pv_init) in %.1f s" % (rank, local_rank, phases["pv_init"]))
     t0 = time.perf_counter()
     db = DeviceBatch(blob, off, pks)
@@ -1080,6 +1094,13 @@ def main():
             "note": "the headline step timed again after ~%.1f s of back-to-back steps (the clock a continuously "
                     "loaded GPU holds; the headline itself follows the driver's warm-up)" % args.sustain_s}
         phases["sustained_load"] = time.perf_counter() - t0
+    hbm_run = hbm_in_use()
+    if hbm_ctx and hbm_run:
+        result["hbm"] = {"context_GB": round(hbm_ctx[0] / 1e9, 2), "with_batch_GB": round(hbm_run[0] / 1e9, 2),
+                         "total_GB": round(hbm_run[1] / 1e9, 1),
+                         "note": "device memory in use after pv_init (the engine context: fixed-base comb, "
+                                 "workspace, staging) and after the batch upload and the timed steps "
+                                 "(hipMemGetInfo, device-wide)"}
     if world > 1:
         result["rccl"] = rccl_summary(world, *comm.rccl_ranks())
     if world > 1 and not args.no_host_path:
