@@ -2293,6 +2293,11 @@ __device__ __forceinline__ void pv_clock_stamp(uint64_t& t, uint64_t& r) {
 #ifndef PV_COMB_AB_PRIO
 #define PV_COMB_AB_PRIO 0
 #endif
+// 0: off; k: the last 1/k of the grid at priority 1. Measured slower (base 393.5-400.9 M/s, last 1/4
+// 391.4-394.6, last 1/8 385.9-397.6: profiles/r06/ab/ab_comb_ab_tail_prio.txt): off
+#ifndef PV_COMB_AB_TAIL_PRIO
+#define PV_COMB_AB_TAIL_PRIO 0
+#endif
 // Workgroup size of the fused comb kernel (A/B knob): its waves share nothing (each stages its own
 // rows in its own 10 KB of LDS), so one-wave workgroups release a slot per wave instead of per four.
 // Measured: 64 within noise of 256, 128 3 % slower (profiles/r06/ab/ab_comb_ab_block.txt); 256 kept.
@@ -2318,6 +2323,9 @@ __global__ __launch_bounds__(PV_COMB_AB_BLOCK, PV_COMB_A_MINBLOCKS) void pv_comb
     const uint4* wkey = pv_kw_rows(kw, i);
 #if PV_COMB_AB_PRIO  // A/B knob: the [S]B phase at a higher issue priority than the [k](-A) phase
     __builtin_amdgcn_s_setprio(PV_COMB_AB_PRIO);
+#endif
+#if PV_COMB_AB_TAIL_PRIO  // A/B knob: the workgroups dispatched last (the final round) at a higher priority
+    if (blockIdx.x >= gridDim.x - gridDim.x / PV_COMB_AB_TAIL_PRIO) __builtin_amdgcn_s_setprio(1);
 #endif
     pv_comb_bw_acc<W>(acc, bcomb, wkey, dig, &stg[wv][0][0]);
 #if PV_COMB_AB_PRIO
