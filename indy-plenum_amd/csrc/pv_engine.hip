@@ -2422,6 +2422,11 @@ struct DevEncSink {
 #ifndef PV_ENC_INV_DUAL
 #define PV_ENC_INV_DUAL 1
 #endif
+// A/B knob: one chain per workgroup (its 4 waves' products shared through LDS). Parity-green; encode stage
+// 0.139-0.141 vs 0.143-0.145 ms, step within noise (profiles/r06/ab/ab_encode_wg_inv.txt): off, no barrier
+#ifndef PV_ENC_WG_INV
+#define PV_ENC_WG_INV 0
+#endif
 __device__ __forceinline__ void pv_shfl_xor_fe(fe& o, const fe& a, int m) {
 #pragma unroll
     for (int k = 0; k < 10; k++) o.v[k] = __shfl_xor(a.v[k], m);
@@ -2440,9 +2445,52 @@ struct PvWaveInvert {
             pv_shfl_xor_fe(q, p[i], M[i]);
             fe_mul(p[i + 1], p[i], q);
         }
-        // row r (lanes 16 r + k) gets limb k of lane (r & RES)'s product
         const LpLane c = LpLane::make();
         const int src = (int)((lane >> 4) & RES);
+        fe inv;
+#if PV_ENC_WG_INV
+        // the workgroup's waves share ONE chain: their (two) products meet in LDS, wave 0 inverts the
+        // workgroup's products, and each wave takes its own inverse as that times the other waves' products
+        static_assert(PV_ENC_INV_DUAL, "PV_ENC_WG_INV: the dual-row form (two products per wave)");
+        constexpr int NW = PV_BLOCK / 64;
+        __shared__ uint32_t wg_p[NW][2][10];
+        __shared__ uint32_t wg_inv[2][10];
+        const uint32_t wv = threadIdx.x >> 6, r = lane & 1u;
+        if (lane < 2) {
+#pragma unroll
+            for (int k = 0; k < 10; k++) wg_p[wv][lane][k] = p[LV].v[k];
+        }
+        __syncthreads();
+        fe others;  // the product of the other waves' products of residue r
+        bool have = false;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            if ((uint32_t)w == wv) continue;
+            fe o;
+#pragma unroll
+            for (int k = 0; k < 10; k++) o.v[k] = wg_p[w][r][k];
+            if (have) fe_mul(others, others, o);
+            else others = o;
+            have = true;
+        }
+        if (wv == 0) {  // wave-uniform
+            fe tot;
+            fe_mul(tot, others, p[LV]);
+            uint32_t z = 0;
+#pragma unroll
+            for (int k = 0; k < 10; k++) {
+                const uint32_t t = __shfl(tot.v[k], src);
+                z = (lane & 15u) == (uint32_t)k ? t : z;
+            }
+            const lu zi = lp_invert<true>(c, lu(z));
+            if ((lane >> 4) < 2u && (lane & 15u) < 10u) wg_inv[lane >> 4][lane & 15u] = static_cast<uint32_t>(zi);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 10; k++) inv.v[k] = wg_inv[r][k];
+        fe_mul(inv, inv, others);
+#else
+        // row r (lanes 16 r + k) gets limb k of lane (r & RES)'s product
         uint32_t z = 0;
 #pragma unroll
         for (int k = 0; k < 10; k++) {
@@ -2450,9 +2498,9 @@ struct PvWaveInvert {
             z = (lane & 15u) == (uint32_t)k ? t : z;
         }
         const lu zi = lp_invert<PV_ENC_INV_DUAL != 0>(c, lu(z));
-        fe inv;
 #pragma unroll
         for (int k = 0; k < 10; k++) inv.v[k] = __shfl(static_cast<uint32_t>(zi), (int)(16u * (lane & RES)) + k);
+#endif
 #pragma unroll
         for (int i = LV - 1; i >= 0; i--) {
             pv_shfl_xor_fe(q, p[i], M[i]);
